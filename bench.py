@@ -1,0 +1,286 @@
+#!/usr/bin/env python
+"""bench.py — BASELINE.json metric: cell-updates/s (+ env-steps/s) of the batched
+ForestFireBulldozer CA on 4096 x (256 x 256) grids per MI355X.
+
+Workload (BASELINE config 3): AdvancedForestFireBulldozerEnv,
+Alexandridis rule, E = 4096 envs per GPU, N = 256, use_hidden=False (veg = den = 3,
+altitude 0 -> p_slope = 1, still read from HBM every step), mid-episode synthetic state
+(grid iid {EMPTY .1, TREE .8, FIRE .1}, fire ages iid [1, 672], wind_index iid [0, 8)),
+p_tree = 0, p_wind_change = 0.06. One timed step = random actions (device Philox) +
+the CA step (gca_alex_step) + the env step (gca_advenv_post) [+ one RCCL all_gather of the
+per-env done mask / reward when --gpus > 1]. Weak scaling: every rank owns E envs.
+
+Also reported: the WindyForestFire bulldozer env (config 2, E = 1024) as `secondary`,
+the roofline of the dominant kernel (HIP events over the timed region) and the CPU
+baseline (the oracle's C restatement, single core, bounded sample).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "gym-cellular-automata_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+ALEX_BYTES_PER_CELL = 41  # grid r+w 2, age r+w 4, veg 1, den 1, p_slope 32, dousing 1
+WINDY_BYTES_PER_CELL = 2  # u8 read + u8 write
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
+    ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--gather", choices=["step", "none"], default="step")
+    ap.add_argument("--no-secondary", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    return ap.parse_args()
+
+
+def setup_dist(args):
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    pg = None
+    if world > 1:
+        import torch.distributed as dist
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+        pg = dist
+    return world, rank, torch.device("cuda", local), pg
+
+
+def synthetic_state(env, rank, device):
+    """C3 mid-episode state, drawn on the device (Philox for the grid)."""
+    import torch
+
+    from gymca_amd import _device as dev
+    from gymca_amd._lib import call
+
+    E, N = env.num_envs, env.nrows
+    cdf = torch.tensor([0.1, 0.9, 1.0], dtype=torch.float32, device=device)
+    vals = torch.tensor([0, 1, 2], dtype=torch.uint8, device=device)
+    grid = torch.empty((E, N, N), dtype=torch.uint8, device=device)
+    call("gca_fill_categorical", dev.ptr(grid), N * N, E, env.env_offset, 1, dev.ptr(cdf), dev.ptr(vals), 3,
+         dev.stream_ptr(device))
+    gen = torch.Generator(device=device).manual_seed(1000 + rank)
+    age = torch.where(grid == 2, torch.randint(1, 673, (E, N, N), device=device, generator=gen, dtype=torch.int16),
+                      torch.zeros((), dtype=torch.int16, device=device))
+    widx = torch.randint(0, 8, (E,), device=device, generator=gen, dtype=torch.int32)
+    env.set_state(grid=grid, fire_age=age, wind_index=widx)
+
+
+def timed_loop(step_fn, K, W, pg, device):
+    import torch
+
+    for _ in range(W):
+        step_fn(None)
+    torch.cuda.synchronize(device)
+    if pg is not None:
+        pg.barrier()
+    torch.cuda.synchronize(device)
+    events = []
+    t0 = time.perf_counter()
+    for _ in range(K):
+        step_fn(events)
+    torch.cuda.synchronize(device)
+    if pg is not None:
+        pg.barrier()
+    torch.cuda.synchronize(device)
+    dt = time.perf_counter() - t0
+    kern = [a.elapsed_time(b) * 1e-3 for a, b in events]
+    if pg is not None:
+        t = torch.tensor([dt], dtype=torch.float64, device=device)
+        pg.all_reduce(t, op=pg.ReduceOp.MAX)
+        dt = float(t.item())
+    return dt, (sum(kern) / len(kern) if kern else None)
+
+
+def bench_alex(args, world, rank, device, pg):
+    import torch
+
+    from gymca_amd import _device as dev
+    from gymca_amd._lib import call
+    from gymca_amd.forest_fire.bulldozer import AdvancedForestFireBulldozerEnv
+
+    E, N = args.envs, args.size
+    env = AdvancedForestFireBulldozerEnv(N, N, key=1, num_envs=E, use_hidden=False, device=device,
+                                         env_offset=rank * E)
+    env.reset()
+    synthetic_state(env, rank, device)
+    action = torch.zeros((E, 2), dtype=torch.int32, device=device)
+    gathered = [torch.empty(E * 5, dtype=torch.uint8, device=device) for _ in range(world)] if world > 1 else None
+    st = dev.stream_ptr(device)
+
+    def step(events):
+        call("gca_random_actions", dev.ptr(action), E, env.env_offset, 7, dev.ptr(env.rng_step), st)
+        if events is not None:
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            env.ca_step()
+            b.record()
+            events.append((a, b))
+        else:
+            env.ca_step()
+        call("gca_advenv_post", env.env_params, dev.ptr(action), dev.ptr(env.pos), dev.ptr(env.accu),
+             dev.ptr(env.wind_index), dev.ptr(env.time_step), dev.ptr(env.is_night), dev.ptr(env.dousing), N, N,
+             dev.ptr(env.counts), dev.ptr(env.rng_step), dev.ptr(env.reward), dev.ptr(env.done), E, st)
+        if gathered is not None and args.gather == "step":
+            # RCCL all-gather of the per-env done mask + reward
+            payload = torch.cat([env.done, env.reward.view(torch.uint8)])
+            pg.all_gather(gathered, payload)
+
+    dt, kern = timed_loop(step, args.steps, args.warmup, pg, device)
+    cells = world * E * N * N * args.steps
+    res = {
+        "value": cells / dt,
+        "env_steps_per_s": world * E * args.steps / dt,
+        "ms_per_step": dt / args.steps * 1e3,
+        "kernel_ms": kern * 1e3,
+        "achieved_gbs": ALEX_BYTES_PER_CELL * E * N * N / kern / 1e9,
+        "fires_left": int((env.counts[:, 2] > 0).sum().item()),
+    }
+    return res
+
+
+def bench_windy(args, world, rank, device, pg):
+    import torch
+
+    from gymca_amd import _device as dev
+    from gymca_amd._lib import call
+    from gymca_amd.forest_fire.bulldozer import BatchedForestFireBulldozerEnv
+
+    E, N = 1024, 256
+    env = BatchedForestFireBulldozerEnv(E, N, N, device=device, seed=0x5EED, env_offset=rank * E,
+                                        materialize_obs=False)
+    env.reset()
+    action = torch.zeros((E, 2), dtype=torch.int32, device=device)
+    st = dev.stream_ptr(device)
+
+    def env_step(events):
+        call("gca_random_actions", dev.ptr(action), E, env.env_offset, 9, dev.ptr(env.rng_step), st)
+        env.step(action)
+
+    K = max(args.steps, 40)
+    dt_env, _ = timed_loop(env_step, K, args.warmup, pg, device)
+    # CA-only (steps[E] = 1 forced), dense variant {0:.1, 3:.6, 25:.3}
+    g = env.grids()
+    u = torch.rand(g.shape, device=device)
+    g = torch.where(u < 0.1, 0, torch.where(u < 0.7, 3, 25)).to(torch.uint8)
+    env.buf[0].copy_(g)
+    env.parity.zero_()
+    env.dir_mask.copy_(torch.randint(0, 256, (E,), dtype=torch.uint8, device=device))
+
+    def ca_step(events):
+        if events is not None:
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            env.ca_step_all()
+            b.record()
+            events.append((a, b))
+        else:
+            env.ca_step_all()
+
+    dt_ca, kern = timed_loop(ca_step, K, args.warmup, pg, device)
+    return {
+        "config": "ForestFireBulldozer 256x256, 1024 envs/GPU, WindyForestFire",
+        "env_steps_per_s": world * E * K / dt_env,
+        "ca_only_cell_updates_per_s": world * E * N * N * K / dt_ca,
+        "ca_kernel_ms": kern * 1e3,
+        "ca_achieved_gbs": WINDY_BYTES_PER_CELL * E * N * N / kern / 1e9,
+        "ca_roofline_frac": WINDY_BYTES_PER_CELL * E * N * N / kern / 1e9 / HBM_PEAK_GBS,
+    }
+
+
+def cpu_baseline(args):
+    """The oracle's C restatement (single core) on a bounded sample of the same workload."""
+    import numpy as np
+
+    from gymca_amd.forest_fire.bulldozer.init_utils import get_winds
+    from gymca_amd.forest_fire.operators.ca_alexandridis import make_alex_params
+    from oracle import alex_c
+
+    N, Es = args.size, 8
+    rng = np.random.default_rng(1)
+    grid = rng.choice(np.array([0, 1, 2], np.uint8), size=(Es, N, N), p=[0.1, 0.8, 0.1])
+    age = np.where(grid == 2, rng.integers(1, 673, (Es, N, N)), 0).astype(np.int16)
+    three = np.full((Es, N, N), 3, np.uint8)
+    dous = np.zeros((Es, N, N), np.uint8)
+    ps = np.ones((Es, 8, N, N), np.float32)
+    widx = rng.integers(0, 8, Es).astype(np.int32)
+    p, _ = make_alex_params(N, 0, 1, 2, np.asarray(get_winds(False), np.float32), 0.0, 1)
+    alex_c.alex_step(p, grid, age, three, three, dous, ps, widx)  # warm
+    steps, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < args.cpu_seconds:
+        grid, age, _, _ = alex_c.alex_step(p, grid, age, three, three, dous, ps, widx,
+                                           rng_step=np.full(Es, steps, np.uint32))
+        steps += 1
+    dt = time.perf_counter() - t0
+    return {"value": Es * N * N * steps / dt, "unit": "cell-updates/s", "cores": 1, "kind": "port",
+            "sample": f"{Es} envs x {N}x{N}, {steps} Alexandridis steps, oracle/gca_oracle.c (gcc -O2, 1 thread)"}
+
+
+def main():
+    args = parse()
+    world, rank, device, pg = setup_dist(args)
+    import torch
+
+    alex = bench_alex(args, world, rank, device, pg)
+    secondary = None if args.no_secondary else bench_windy(args, world, rank, device, pg)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args)
+    traffic = None
+    tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(tf):
+        try:
+            traffic = json.load(open(tf)).get("alex_step_bytes_per_launch")
+        except (ValueError, OSError):
+            traffic = None
+    if rank == 0:
+        out = {
+            "metric": "cell-updates/sec, 4096x(256x256) ForestFireBulldozer (Alexandridis CA), per-GPU batch",
+            "value": alex["value"],
+            "unit": "cell-updates/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": alex["ms_per_step"],
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8 cells / i16 ages / f32 probabilities",
+            "data": "synthetic (device Philox mid-episode state, SURVEY.md §8d C3)",
+            "config": {"workload": "AdvancedForestFireBulldozer 256x256, 4096 envs/GPU, Alexandridis rule, "
+                                   "use_hidden=False (BASELINE config 3)",
+                       "envs_per_gpu": args.envs, "grid": [args.size, args.size],
+                       "parallelism": f"env-sharded x{world}" + (", RCCL all_gather done/reward per step"
+                                                                  if world > 1 and args.gather == "step" else "")},
+            "env_steps_per_s": alex["env_steps_per_s"],
+            "roofline": {"bound": "hbm", "achieved": alex["achieved_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": alex["achieved_gbs"] / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "alex_step_kernel", "kernel_ms": alex["kernel_ms"],
+                         "algorithmic_bytes_per_cell": ALEX_BYTES_PER_CELL},
+            "cpu_baseline": cpu,
+            "secondary": secondary,
+        }
+        print(json.dumps(out))
+    if pg is not None:
+        pg.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

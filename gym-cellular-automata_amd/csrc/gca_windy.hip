@@ -1,0 +1,300 @@
+// gca_windy.hip — WindyForestFire CA step on gfx950 (reference: ca_windy.py:41-139).
+//
+// Reference semantics (scipy.signal.convolve2d, mode="same", boundary fill = empty):
+//   S[r,c] = 2048*x[r,c] + sum_{(a,b)!=(1,1)} K[a,b] * x[r-(a-1), c-(b-1)]
+//   K[a,b] = 8 if direction (a,b) is active this step (roll < wind), else `empty`.
+//   new = EMPTY (S<2048T) | TREE (S<2048T+8F) | FIRE (S<2048F) | EMPTY.
+// Direction bit d of dir_mask indexes (a,b) row-major with the centre skipped.
+//
+// Two kernels:
+//  * windy_exact_kernel : the formula above, literally, one thread per cell. Any H, W,
+//    any u8 cell codes (covers empty != 0, where failed directions still weigh `empty`).
+//  * windy_fast_kernel  : empty == 0 and W = 16*LPR (LPR | 64). Then, for grids whose
+//    cells are in {0,T,F} (checked at the boundary) and the constructor's asserted
+//    ordering (ca_windy.py:141-173), the thresholds reduce EXACTLY to
+//      TREE -> FIRE iff some active direction sees FIRE;  FIRE -> EMPTY;  else unchanged.
+//    Each lane owns 16 consecutive cells (one 16-B load/store per row), a wave covers
+//    RPW = 64/LPR rows per step and marches down a strip of SH rows. Fire flags are
+//    SWAR bytes; vertical neighbours come from the adjacent lane group (ds_bpermute),
+//    horizontal ones from byte funnel shifts plus the neighbour lane's edge dword.
+//    Reward/done counts of the new grid are fused (wave reduction + 3 atomics).
+#include "gca_common.h"
+
+// ------------------------------------------------------------------ dir mask
+__global__ void windy_dirmask_kernel(const double* __restrict__ wind, int64_t wind_stride,
+                                     const double* __restrict__ roll, uint32_t k0, uint32_t k1,
+                                     const uint32_t* __restrict__ rng_step, const int32_t* __restrict__ steps,
+                                     int pass, int env_offset, uint8_t* __restrict__ dir_mask, int E) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= E) return;
+    if (steps && steps[e] <= pass) return;
+    const uint32_t step = (rng_step ? rng_step[e] : 0u) + (uint32_t)pass;
+    dir_mask[e] = (uint8_t)windy_mask(wind + (int64_t)e * wind_stride, roll ? roll + (int64_t)e * 9 : nullptr, k0, k1,
+                                      (uint32_t)(env_offset + e), step);
+}
+
+// ------------------------------------------------------------------ exact kernel
+__global__ __launch_bounds__(256) void windy_exact_kernel(uint8_t* __restrict__ buf0, uint8_t* __restrict__ buf1,
+                                                          const uint8_t* __restrict__ parity,
+                                                          const int32_t* __restrict__ steps, int pass,
+                                                          const uint8_t* __restrict__ dir_mask, int E, int H, int W,
+                                                          int empty, int tree, int fire, int32_t* __restrict__ counts) {
+    const int64_t HW = (int64_t)H * W;
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool in_range = idx < (int64_t)E * HW;
+    const int e = in_range ? (int)(idx / HW) : E - 1;
+    const bool active = in_range && (!steps || steps[e] > pass);
+    int out_code = -1;
+    if (active) {
+        const int64_t cell = idx - (int64_t)e * HW;
+        const int r = (int)(cell / W), c = (int)(cell - (int64_t)r * W);
+        const bool odd = parity && parity[e];
+        const uint8_t* src = (odd ? buf1 : buf0) + (int64_t)e * HW;
+        uint8_t* dst = (odd ? buf0 : buf1) + (int64_t)e * HW;
+        const uint32_t m = dir_mask[e];
+        int32_t S = 2048 * (int32_t)src[cell];
+        int d = 0;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+#pragma unroll
+            for (int b = 0; b < 3; ++b) {
+                if (a == 1 && b == 1) continue;
+                const int sr = r - (a - 1), sc = c - (b - 1);
+                const int32_t nb = (sr >= 0 && sr < H && sc >= 0 && sc < W) ? (int32_t)src[(int64_t)sr * W + sc] : empty;
+                const int32_t k = ((m >> d) & 1u) ? 8 : empty;
+                S += k * nb;
+                ++d;
+            }
+        }
+        const int32_t keep = 2048 * tree, prop = 2048 * tree + 8 * fire, cons = 2048 * fire;
+        int v = empty;
+        if (S >= keep && S < prop) v = tree;
+        if (S >= prop && S < cons) v = fire;
+        if (S >= cons) v = empty;
+        dst[cell] = (uint8_t)v;
+        out_code = v;
+    }
+    if (counts) {
+        // waves whose lanes all belong to one env reduce first; mixed waves fall back to per-lane atomics
+        const int e0 = __shfl(e, 0), e63 = __shfl(e, 63);
+        const bool uniform = (e0 == e63) && __all(active || !in_range);
+        if (uniform) {
+            const int nE = __popcll(__ballot(out_code == empty));
+            const int nT = __popcll(__ballot(out_code == tree && tree != empty));
+            const int nF = __popcll(__ballot(out_code == fire));
+            if ((threadIdx.x & 63) == 0 && __any(active)) {
+                atomicAdd(counts + 3 * e0 + 0, nE);
+                atomicAdd(counts + 3 * e0 + 1, nT);
+                atomicAdd(counts + 3 * e0 + 2, nF);
+            }
+        } else if (active) {
+            if (out_code == empty) atomicAdd(counts + 3 * e + 0, 1);
+            else if (out_code == tree) atomicAdd(counts + 3 * e + 1, 1);
+            else if (out_code == fire) atomicAdd(counts + 3 * e + 2, 1);
+        }
+    }
+}
+
+// ------------------------------------------------------------------ fast kernel
+struct Row16 {
+    uint32_t f[4];  // 0x01 per byte where cell == FIRE
+    uint32_t t[4];  // 0x01 per byte where cell == TREE
+};
+
+__device__ __forceinline__ Row16 classify(uint4 v, uint32_t Tp, uint32_t Fp, bool valid) {
+    Row16 o;
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        o.f[j] = valid ? bytes_eq01(w[j], Fp) : 0u;
+        o.t[j] = valid ? bytes_eq01(w[j], Tp) : 0u;
+    }
+    return o;
+}
+
+__device__ __forceinline__ uint32_t shfl_u32(uint32_t v, int src_lane) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane << 2, (int)v);
+}
+
+template <int LPR>
+__global__ __launch_bounds__(256) void windy_fast_kernel(uint8_t* __restrict__ buf0, uint8_t* __restrict__ buf1,
+                                                         const uint8_t* __restrict__ parity,
+                                                         const int32_t* __restrict__ steps, int pass,
+                                                         const uint8_t* __restrict__ dir_mask, int H, int SH,
+                                                         int blocks_per_env, uint32_t Ep, uint32_t Tp, uint32_t Fp,
+                                                         int32_t* __restrict__ counts) {
+    constexpr int W = 16 * LPR;
+    constexpr int RPW = 64 / LPR;
+    const int env = blockIdx.x / blocks_per_env;
+    const int sblk = blockIdx.x - env * blocks_per_env;
+    if (steps && steps[env] <= pass) return;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int g = lane / LPR, q = lane - g * LPR;
+    const int s0 = (sblk * 4 + wave) * SH;
+    if (s0 >= H) return;
+    const int s_end = min(s0 + SH, H);
+    const int nT = (s_end - s0 + RPW - 1) / RPW;
+
+    const bool odd = parity && parity[env];
+    const int64_t HW = (int64_t)H * W;
+    const uint8_t* __restrict__ S = (odd ? buf1 : buf0) + (int64_t)env * HW + 16 * q;
+    uint8_t* __restrict__ D = (odd ? buf0 : buf1) + (int64_t)env * HW + 16 * q;
+
+    const uint32_t m = dir_mask[env];
+    const uint32_t m0 = (m & 1u) ? ~0u : 0u, m1 = (m & 2u) ? ~0u : 0u, m2 = (m & 4u) ? ~0u : 0u,
+                   m3 = (m & 8u) ? ~0u : 0u, m4 = (m & 16u) ? ~0u : 0u, m5 = (m & 32u) ? ~0u : 0u,
+                   m6 = (m & 64u) ? ~0u : 0u, m7 = (m & 128u) ? ~0u : 0u;
+
+    auto load_row = [&](int R, bool want) -> uint4 {
+        if (want && R >= 0 && R < H) return *reinterpret_cast<const uint4*>(S + (int64_t)R * W);
+        return make_uint4(0u, 0u, 0u, 0u);
+    };
+
+    // prologue: chunk -1 (only the row just above the strip), chunk 0, chunk 1 in flight
+    const int Rprev = s0 - RPW + g;
+    Row16 prv = classify(load_row(Rprev, g == RPW - 1), Tp, Fp, g == RPW - 1 && Rprev >= 0);
+    int Rc = s0 + g;
+    Row16 cur = classify(load_row(Rc, true), Tp, Fp, Rc < H);
+    int Rn = s0 + RPW + g;
+    uint4 raw_next = load_row(Rn, nT > 1 || g == 0);
+
+    const int lane_up = (lane - LPR) & 63, lane_dn = (lane + LPR) & 63;
+    const int lane_l = (lane - 1) & 63, lane_r = (lane + 1) & 63;
+    const bool has_l = q > 0, has_r = q < LPR - 1;
+
+    int32_t cntT = 0, cntF = 0, cntV = 0;
+    for (int t = 0; t < nT; ++t) {
+        const bool next_wanted = (t + 1 < nT) || g == 0;
+        Row16 nxt = classify(raw_next, Tp, Fp, next_wanted && Rn < H);
+        // issue the load two chunks ahead before computing this chunk
+        const int Rn2 = Rn + RPW;
+        raw_next = load_row(Rn2, (t + 2 < nT) || (t + 2 == nT && g == 0));
+
+        uint32_t up[4], dn[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            up[j] = shfl_u32(g == RPW - 1 ? prv.f[j] : cur.f[j], lane_up);
+            dn[j] = shfl_u32(g == 0 ? nxt.f[j] : cur.f[j], lane_dn);
+        }
+        // edge dwords of the neighbouring 16-cell chunks (same row) for +-1 column shifts
+        // (bpermutes run in every lane: a lane switched off in EXEC would not serve its value)
+        const uint32_t s_upL = shfl_u32(up[3], lane_l), s_upR = shfl_u32(up[0], lane_r);
+        const uint32_t s_cuL = shfl_u32(cur.f[3], lane_l), s_cuR = shfl_u32(cur.f[0], lane_r);
+        const uint32_t s_dnL = shfl_u32(dn[3], lane_l), s_dnR = shfl_u32(dn[0], lane_r);
+        const uint32_t upL = has_l ? s_upL : 0u, upR = has_r ? s_upR : 0u;
+        const uint32_t cuL = has_l ? s_cuL : 0u, cuR = has_r ? s_cuR : 0u;
+        const uint32_t dnL = has_l ? s_dnL : 0u, dnR = has_r ? s_dnR : 0u;
+
+        uint32_t outw[4];
+        int32_t rowT = 0, rowF = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            // X_l: byte i holds X[i-1] (source column c-1); X_r: byte i holds X[i+1] (column c+1)
+            const uint32_t up_l = __builtin_amdgcn_alignbyte(up[j], j ? up[j - 1] : upL, 3);
+            const uint32_t up_r = __builtin_amdgcn_alignbyte(j < 3 ? up[j + 1] : upR, up[j], 1);
+            const uint32_t cu_l = __builtin_amdgcn_alignbyte(cur.f[j], j ? cur.f[j - 1] : cuL, 3);
+            const uint32_t cu_r = __builtin_amdgcn_alignbyte(j < 3 ? cur.f[j + 1] : cuR, cur.f[j], 1);
+            const uint32_t dn_l = __builtin_amdgcn_alignbyte(dn[j], j ? dn[j - 1] : dnL, 3);
+            const uint32_t dn_r = __builtin_amdgcn_alignbyte(j < 3 ? dn[j + 1] : dnR, dn[j], 1);
+            // d -> source (r+1-a, c+1-b): d0 down/c+1, d1 down, d2 down/c-1, d3 cur/c+1,
+            //                             d4 cur/c-1, d5 up/c+1, d6 up, d7 up/c-1
+            const uint32_t any = (dn_r & m0) | (dn[j] & m1) | (dn_l & m2) | (cu_r & m3) | (cu_l & m4) |
+                                 (up_r & m5) | (up[j] & m6) | (up_l & m7);
+            const uint32_t ign = cur.t[j] & any;          // TREE -> FIRE
+            const uint32_t keep = cur.t[j] & ~any;        // TREE stays
+            const uint32_t ignm = (ign << 8) - ign;       // 0x01 -> 0xFF per byte
+            const uint32_t keepm = (keep << 8) - keep;
+            outw[j] = (ignm & Fp) | (keepm & Tp) | (~(ignm | keepm) & Ep);
+            rowF += __popc(ign);
+            rowT += __popc(keep);
+        }
+        if (Rc < s_end) {  // rows of the last partial chunk past the strip are neither stored nor counted
+            *reinterpret_cast<uint4*>(D + (int64_t)Rc * W) = make_uint4(outw[0], outw[1], outw[2], outw[3]);
+            cntV += 16;
+            cntT += rowT;
+            cntF += rowF;
+        }
+        prv = cur;
+        cur = nxt;
+        Rc = Rn;
+        Rn = Rn2;
+    }
+    if (counts) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            cntT += __shfl_xor(cntT, off);
+            cntF += __shfl_xor(cntF, off);
+            cntV += __shfl_xor(cntV, off);
+        }
+        if (lane == 0) {
+            atomicAdd(counts + 3 * env + 0, cntV - cntT - cntF);
+            atomicAdd(counts + 3 * env + 1, cntT);
+            atomicAdd(counts + 3 * env + 2, cntF);
+        }
+    }
+}
+
+// ------------------------------------------------------------------ host API
+extern "C" int gca_windy_dirmask(const double* wind, int64_t wind_stride, const double* roll, uint64_t seed,
+                                 const uint32_t* rng_step, const int32_t* steps, int pass, int env_offset,
+                                 uint8_t* dir_mask, int E, void* stream) {
+    GCA_CHECK_ARG(E > 0 && wind && dir_mask, "E > 0, wind and dir_mask required");
+    GCA_CHECK_ARG(wind_stride >= 0, "wind_stride >= 0");
+    const int threads = 256, blocks = (E + threads - 1) / threads;
+    hipLaunchKernelGGL(windy_dirmask_kernel, dim3(blocks), dim3(threads), 0, (hipStream_t)stream, wind, wind_stride,
+                       roll, (uint32_t)seed, (uint32_t)(seed >> 32), rng_step, steps, pass, env_offset, dir_mask, E);
+    GCA_CHECK_LAUNCH("windy_dirmask");
+    return GCA_OK;
+}
+
+template <int LPR>
+static void launch_fast(uint8_t* b0, uint8_t* b1, const uint8_t* parity, const int32_t* steps, int pass,
+                        const uint8_t* dm, int E, int H, int empty, int tree, int fire, int32_t* counts,
+                        hipStream_t st) {
+    constexpr int RPW = 64 / LPR;
+    // strip height: >= 32 rows when there is enough work, multiple of RPW
+    const int64_t rows = (int64_t)E * H;
+    int SH = 32;
+    while (SH > RPW && rows / SH < 8192) SH >>= 1;
+    if (SH < RPW) SH = RPW;
+    SH = ((SH + RPW - 1) / RPW) * RPW;
+    const int strips = (H + SH - 1) / SH;
+    const int bpe = (strips + 3) / 4;
+    hipLaunchKernelGGL(windy_fast_kernel<LPR>, dim3((unsigned)((int64_t)E * bpe)), dim3(256), 0, st, b0, b1, parity,
+                       steps, pass, dm, H, SH, bpe, rep4(empty), rep4(tree), rep4(fire), counts);
+}
+
+extern "C" int gca_windy_step(uint8_t* buf0, uint8_t* buf1, const uint8_t* parity, const int32_t* steps, int pass,
+                              const uint8_t* dir_mask, int E, int H, int W, int empty, int tree, int fire,
+                              int force_exact, int32_t* counts, void* stream) {
+    GCA_CHECK_ARG(buf0 && buf1 && dir_mask, "buffers and dir_mask required");
+    GCA_CHECK_ARG(E > 0 && H > 0 && W > 0, "E, H, W must be positive");
+    GCA_CHECK_ARG(empty >= 0 && empty < 256 && tree >= 0 && tree < 256 && fire >= 0 && fire < 256,
+                  "cell codes must fit in u8");
+    GCA_CHECK_ARG(empty < tree && tree < fire, "cell codes must satisfy empty < tree < fire (ca_windy.py:158)");
+    hipStream_t st = (hipStream_t)stream;
+    const bool aligned = ((((uintptr_t)buf0) | ((uintptr_t)buf1)) & 15u) == 0;
+    const int LPR = W / 16;
+    const bool fast = !force_exact && empty == 0 && aligned && (W % 16 == 0) && LPR >= 1 && LPR <= 64 && (64 % LPR) == 0;
+    if (fast) {
+        switch (LPR) {
+            case 1: launch_fast<1>(buf0, buf1, parity, steps, pass, dir_mask, E, H, empty, tree, fire, counts, st); break;
+            case 2: launch_fast<2>(buf0, buf1, parity, steps, pass, dir_mask, E, H, empty, tree, fire, counts, st); break;
+            case 4: launch_fast<4>(buf0, buf1, parity, steps, pass, dir_mask, E, H, empty, tree, fire, counts, st); break;
+            case 8: launch_fast<8>(buf0, buf1, parity, steps, pass, dir_mask, E, H, empty, tree, fire, counts, st); break;
+            case 16: launch_fast<16>(buf0, buf1, parity, steps, pass, dir_mask, E, H, empty, tree, fire, counts, st); break;
+            case 32: launch_fast<32>(buf0, buf1, parity, steps, pass, dir_mask, E, H, empty, tree, fire, counts, st); break;
+            case 64: launch_fast<64>(buf0, buf1, parity, steps, pass, dir_mask, E, H, empty, tree, fire, counts, st); break;
+        }
+        GCA_CHECK_LAUNCH("windy_fast");
+    } else {
+        const int64_t n = (int64_t)E * H * W;
+        const int threads = 256;
+        const int64_t blocks = (n + threads - 1) / threads;
+        GCA_CHECK_ARG(blocks < (int64_t)1 << 31, "grid too large for the exact kernel");
+        hipLaunchKernelGGL(windy_exact_kernel, dim3((unsigned)blocks), dim3(threads), 0, st, buf0, buf1, parity, steps,
+                           pass, dir_mask, E, H, W, empty, tree, fire, counts);
+        GCA_CHECK_LAUNCH("windy_exact");
+    }
+    return GCA_OK;
+}

@@ -1,0 +1,148 @@
+"""ctypes binding of libgca_hip.so — the C-ABI declared in include/gca.h.
+
+This module is the ONLY bridge between Python and the gfx950 kernels. It fails
+loudly (GCAError at import of a product op) when the shared library is missing:
+there is no CPU fallback anywhere in the product path.
+"""
+import ctypes
+import os
+from ctypes import POINTER, c_double, c_float, c_int, c_int16, c_int32, c_int64, c_uint32, c_uint64, c_void_p
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libgca_hip.so")
+
+GCA_OK = 0
+GCA_MAX_RADIUS = 8
+
+TAG_WINDY_ROLL = 0x574E4459
+TAG_ALEX_CELL = 0x414C5843
+TAG_ALEX_WIND = 0x414C5857
+TAG_ACTION = 0x41435449
+TAG_INIT = 0x494E4954
+TAG_DS_CELL = 0x44534345
+
+
+class GCAError(RuntimeError):
+    """Raised when the HIP library is missing or a C-ABI call returns non-zero."""
+
+
+class BulldozerParams(ctypes.Structure):
+    """gca_bulldozer_params (include/gca.h)."""
+
+    _fields_ = [
+        ("t_move", c_double * 9),
+        ("t_shoot", c_double * 2),
+        ("t_any", c_double),
+        ("seed", c_uint64),
+        ("env_offset", c_int32),
+        ("empty", c_int32),
+        ("tree", c_int32),
+        ("fire", c_int32),
+        ("up_mask", c_int32),
+        ("down_mask", c_int32),
+        ("left_mask", c_int32),
+        ("right_mask", c_int32),
+        ("effect", c_int16 * 256),
+    ]
+
+
+class AlexParams(ctypes.Structure):
+    """gca_alex_params (include/gca.h)."""
+
+    _fields_ = [
+        ("R", c_int32),
+        ("heat_dw", c_float * (GCA_MAX_RADIUS + 1)),
+        ("dous_inner", c_float),
+        ("dous_border", c_float),
+        ("veg1p", c_float * 6),
+        ("den1p", c_float * 6),
+        ("p_tree", c_float),
+        ("age_lo", c_int32),
+        ("age_hi", c_int32),
+        ("seed", c_uint64),
+        ("env_offset", c_int32),
+        ("empty", c_int32),
+        ("tree", c_int32),
+        ("fire", c_int32),
+        ("n_winds", c_int32),
+        ("winds", (c_float * 9) * 16),
+    ]
+
+
+class AdvEnvParams(ctypes.Structure):
+    """gca_advenv_params (include/gca.h)."""
+
+    _fields_ = [
+        ("t_move", c_float * 9),
+        ("t_shoot", c_float * 2),
+        ("t_any", c_float),
+        ("p_wind_change", c_float),
+        ("day_length", c_int32),
+        ("seed", c_uint64),
+        ("env_offset", c_int32),
+        ("n_winds", c_int32),
+        ("up_mask", c_int32),
+        ("down_mask", c_int32),
+        ("left_mask", c_int32),
+        ("right_mask", c_int32),
+    ]
+
+
+P = c_void_p  # device pointers travel as plain addresses
+_SIGNATURES = {
+    "gca_last_error": ([], ctypes.c_char_p),
+    "gca_version": ([], c_int),
+    "gca_philox": ([P, c_uint32, c_uint32, P, c_int64, P], c_int),
+    "gca_count_cells": ([P, c_int, c_int, c_int, c_int, c_int, c_int, P, P], c_int),
+    "gca_windy_dirmask": ([P, c_int64, P, c_uint64, P, P, c_int, c_int, P, c_int, P], c_int),
+    "gca_windy_step": ([P, P, P, P, c_int, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, P], c_int),
+    "gca_bulldozer_pre": ([POINTER(BulldozerParams), P, P, P, P, P, c_int64, P, P, P, c_int, P], c_int),
+    "gca_bulldozer_interpass": ([POINTER(BulldozerParams), c_int, P, P, P, c_int64, P, P, c_int, P], c_int),
+    "gca_bulldozer_post": ([POINTER(BulldozerParams), c_int, P, P, P, P, P, c_int, c_int, P, P, P, P, P, P, c_int, P],
+                           c_int),
+    "gca_move_modify": ([POINTER(BulldozerParams), P, P, P, c_int, c_int, P, c_int, P], c_int),
+    "gca_alex_prepare_slope": ([P, P, c_int, c_int, c_int, P], c_int),
+    "gca_alex_step": ([POINTER(AlexParams), c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
+                      c_int),
+    "gca_alex_wind_change": ([c_float, c_int, c_uint64, c_int, P, P, P, P, c_int, P], c_int),
+    "gca_alex_slope_from_altitude": ([P, P, P, c_int, c_int, c_int, P], c_int),
+    "gca_advenv_post": ([POINTER(AdvEnvParams), P, P, P, P, P, P, P, c_int, c_int, P, P, P, P, c_int, P], c_int),
+    "gca_reset_where": ([P, c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, P, P], c_int),
+    "gca_fill_categorical": ([P, c_int64, c_int, c_int, c_uint64, P, P, c_int, P], c_int),
+    "gca_random_actions": ([P, c_int, c_int, c_uint64, P, P], c_int),
+    "gca_ds_count_draws": ([P, c_int, c_int, c_int, c_int, c_int, c_int, P, P], c_int),
+    "gca_ds_step": ([P, P, c_int, c_int, c_int, c_int, c_int, c_int, P, P, P, c_uint64, P, c_int, P, P], c_int),
+}
+
+EXPORTED_SYMBOLS = tuple(_SIGNATURES)
+
+_lib = None
+
+
+def load():
+    """Load libgca_hip.so once; raise GCAError if it is not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise GCAError(
+            f"{LIB_PATH} not found: build it with `make -C gym-cellular-automata_amd/csrc` "
+            "(or __graft_entry__.build()). There is no CPU fallback."
+        )
+    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_LOCAL)
+    for name, (argtypes, restype) in _SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = restype
+    _lib = lib
+    return lib
+
+
+def call(name, *args):
+    """Call a gca_* entry point and raise GCAError on a non-zero status."""
+    lib = load()
+    status = getattr(lib, name)(*args)
+    if status != GCA_OK:
+        msg = lib.gca_last_error().decode(errors="replace")
+        raise GCAError(f"{name} failed (status {status}): {msg}")
+    return status

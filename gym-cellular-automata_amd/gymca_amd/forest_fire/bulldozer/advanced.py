@@ -1,0 +1,245 @@
+"""AdvancedForestFireBulldozerEnv — the batched Alexandridis env, resident in HBM.
+
+Reference: advanced_bulldozer.py:63-1133 (JAX, vmap over num_envs). One env step is
+
+    gca_alex_step     RepeatCAJax's single CA step (repeat_ca_jax.py:218-220) of
+                      PartiallyObservableForestFireJax._update_grid (ca_alexandridis_jax.py:321-424),
+                      new-grid tree/fire counts fused
+    gca_advenv_post   wind change (:442-451), f32 time accumulation (repeat_ca_jax.py:191-198),
+                      MoveJax/ModifyJax (move_modify_jax.py:39-157), time_step/is_night
+                      (advanced_bulldozer.py:1116-1127), reward -(f/(t+f+1e-8)) and done (:597-633)
+
+and `conditional_reset` (:422-518) re-injects the initial state of finished envs with
+gca_reset_where. Observations (RGB / extension channels, :988-1101) are the next row
+of SURVEY.md §8f and are not built here: `obs` carries the true grid.
+
+Device layout per env: grid u8 (ping-pong), fire_age i16 (ping-pong), vegetation /
+density / dousing u8, p_slope f32 [8][H][W] (= exp(0.078*slope), computed once at
+reset), plus per-env scalars. 41 B of HBM traffic per cell-update.
+"""
+import numpy as np
+
+from ... import _device as dev
+from ..._lib import AdvEnvParams, call
+from ..operators.ca_alexandridis import alex_constants, make_alex_params
+from .bulldozer import ACTION_SETS, bulldozer_timings
+from .init_utils import get_winds, init_altitude, init_density, init_vegetation
+
+
+class AdvancedForestFireBulldozerEnv:
+    def __init__(self, nrows, ncols, key=0, num_envs=8, speed_move=0.12, speed_act=0.03, speed_multiplier=1.0,
+                 pos_bull=None, pos_fire=None, t_move=None, t_shoot=None, t_any=0.001, p_tree=0.90, p_empty=0.10,
+                 use_hidden=True, middle_fire=False, enable_extensions=False, device=None, env_offset=0):
+        import torch
+
+        self.device = dev.require_device(device)
+        self.nrows, self.ncols, self.num_envs = int(nrows), int(ncols), int(num_envs)
+        E, H, W = self.num_envs, self.nrows, self.ncols
+        self.key = int(key)
+        self.env_offset = int(env_offset)
+        self.use_hidden = use_hidden
+        self.middle_fire = middle_fire
+        self._empty, self._tree, self._fire = 0, 1, 2
+        self._p_tree_init, self._p_empty_init = p_tree, p_empty
+        self._pos_bull = pos_bull
+        self._pos_fire = pos_fire
+        self._p_fire = 0.00033
+        self._p_tree = 0.0  # advanced_bulldozer.py:209
+        self._p_wind_change = 0.06
+        self._day_length = 400
+        self._winds = np.asarray(get_winds(use_hidden), dtype=np.float32)  # (8, 2, 3, 3)
+        t_act_move, t_act_shoot = bulldozer_timings(H, W, speed_move, speed_act, t_move, t_shoot, t_any)
+        self.alex_params, self.constants = make_alex_params(H, self._empty, self._tree, self._fire, self._winds,
+                                                            self._p_tree, self.key, self.env_offset)
+        ep = AdvEnvParams()
+        for a in range(9):  # all moves, not_move included, cost t_move (:753-754)
+            ep.t_move[a] = float(np.float32(t_act_move))
+        ep.t_shoot[0] = ep.t_shoot[1] = float(np.float32(t_act_shoot))
+        ep.t_any = float(np.float32(t_any))
+        ep.p_wind_change = float(np.float32(self._p_wind_change))
+        ep.day_length = self._day_length
+        ep.seed = self.key & (2**64 - 1)
+        ep.env_offset = self.env_offset
+        ep.n_winds = len(self._winds)
+        from ..operators.move_modify import make_params
+
+        mp = make_params(ACTION_SETS)
+        ep.up_mask, ep.down_mask, ep.left_mask, ep.right_mask = mp.up_mask, mp.down_mask, mp.left_mask, mp.right_mask
+        self.env_params = ep
+
+        kw = dict(device=self.device)
+        self.grid = torch.zeros((2, E, H, W), dtype=torch.uint8, **kw)
+        self.age = torch.zeros((2, E, H, W), dtype=torch.int16, **kw)
+        self.cur = 0
+        self.vegetation = torch.full((E, H, W), 3, dtype=torch.uint8, **kw)
+        self.density = torch.full((E, H, W), 3, dtype=torch.uint8, **kw)
+        self.dousing = torch.zeros((E, H, W), dtype=torch.uint8, **kw)
+        self.p_slope = torch.ones((E, 8, H, W), dtype=torch.float32, **kw)
+        self.wind_index = torch.zeros(E, dtype=torch.int32, **kw)
+        self.pos = torch.zeros((E, 2), dtype=torch.int32, **kw)
+        self.accu = torch.zeros(E, dtype=torch.float32, **kw)
+        self.time_step = torch.ones(E, dtype=torch.int32, **kw)
+        self.is_night = torch.zeros(E, dtype=torch.int32, **kw)
+        self.rng_step = torch.zeros(E, dtype=torch.int32, **kw)
+        self.counts = torch.zeros((E, 3), dtype=torch.int32, **kw)
+        self.reward = torch.zeros(E, dtype=torch.float32, **kw)
+        self.done = torch.zeros(E, dtype=torch.uint8, **kw)
+        self.steps_elapsed = torch.zeros(E, dtype=torch.float32, **kw)
+        self.reward_accumulated = torch.zeros(E, dtype=torch.float32, **kw)
+        self._initial = None
+
+    # ------------------------------------------------------------------ init
+    def _hidden_layers(self, rng):
+        """density / vegetation / altitude (:182-197): init_utils restatement when use_hidden."""
+        E, H, W = self.num_envs, self.nrows, self.ncols
+        if self.use_hidden:
+            return init_density(H, W, E, rng), init_vegetation(H, W, E, rng), init_altitude(H, W, E, rng)
+        return None, None, None
+
+    def reset(self, seed=None, options=None):
+        """Initial state of advanced_bulldozer.py:650-743 for every env."""
+        import torch
+
+        E, H, W = self.num_envs, self.nrows, self.ncols
+        st = dev.stream_ptr(self.device)
+        rng = np.random.default_rng(self.key if seed is None else seed)
+        den, veg, alt = self._hidden_layers(rng)
+        if den is not None:
+            self.density.copy_(torch.as_tensor(np.clip(den, 0, 255).astype(np.uint8), device=self.device))
+            self.vegetation.copy_(torch.as_tensor(np.clip(veg, 0, 255).astype(np.uint8), device=self.device))
+            alt_d = torch.as_tensor(alt.astype(np.float64), device=self.device)
+        else:
+            self.density.fill_(3)
+            self.vegetation.fill_(3)
+            alt_d = None
+        call("gca_alex_slope_from_altitude", dev.ptr(alt_d), dev.ptr(self.p_slope), None, E, H, W, st)
+        # grid iid over {EMPTY, TREE} (p_empty, p_tree), two fires with age (N + N//2) * 2 (:650-688)
+        cdf = torch.tensor([self._p_empty_init, self._p_empty_init + self._p_tree_init, 1.0], dtype=torch.float32,
+                           device=self.device)
+        vals = torch.tensor([self._empty, self._tree, self._fire], dtype=torch.uint8, device=self.device)
+        self.cur = 0
+        call("gca_fill_categorical", dev.ptr(self.grid[0]), H * W, E, self.env_offset,
+             (self.key if seed is None else int(seed)) & (2**64 - 1), dev.ptr(cdf), dev.ptr(vals), 3, st)
+        self.age[0].zero_()
+        if self._pos_fire is not None:
+            r, c = self._pos_fire
+        elif self.middle_fire:
+            r, c = H // 2, W // 2
+        else:
+            r, c = 3 * H // 4, W // 4
+        age0 = (H + H // 2) * 2
+        for cc in (c, c - 1):
+            self.grid[0][:, r, cc] = self._fire
+            self.age[0][:, r, cc] = age0
+        br, bc = (int(H * 0.15), int(W * 0.85)) if self._pos_bull is None else self._pos_bull
+        self.pos[:, 0], self.pos[:, 1] = br, bc
+        wi = rng.integers(0, 8, size=E) if self.use_hidden else np.zeros(E)
+        self.wind_index.copy_(torch.as_tensor(wi.astype(np.int32), device=self.device))
+        self.dousing.zero_()
+        self.accu.zero_()
+        self.time_step.fill_(1)
+        self.is_night.zero_()
+        self.rng_step.zero_()
+        self.done.zero_()
+        self.steps_elapsed.zero_()
+        self.reward_accumulated.zero_()
+        call("gca_count_cells", dev.ptr(self.grid[0]), E, H, W, self._empty, self._tree, self._fire,
+             dev.ptr(self.counts), st)
+        self._initial = dict(grid=self.grid[0].clone(), age=self.age[0].clone(), pos=self.pos.clone(),
+                             wind_index=self.wind_index.clone(), counts=self.counts.clone())
+        return self._obs(), self._info()
+
+    def set_state(self, grid=None, fire_age=None, vegetation=None, density=None, wind_index=None, dousing=None,
+                  altitude=None, position=None):
+        """Overwrite parts of the device state (synthetic mid-episode states for benches/tests)."""
+        import torch
+
+        E, H, W = self.num_envs, self.nrows, self.ncols
+        st = dev.stream_ptr(self.device)
+
+        def put(dst, x, dtype):
+            dst.copy_(x.to(dst.device, dtype) if dev.is_device_tensor(x) else torch.as_tensor(np.asarray(x), dtype=dtype,
+                                                                                           device=self.device))
+
+        if grid is not None:
+            put(self.grid[self.cur], grid, torch.uint8)
+        if fire_age is not None:
+            put(self.age[self.cur], fire_age, torch.int16)
+        if vegetation is not None:
+            put(self.vegetation, vegetation, torch.uint8)
+        if density is not None:
+            put(self.density, density, torch.uint8)
+        if wind_index is not None:
+            put(self.wind_index, wind_index, torch.int32)
+        if dousing is not None:
+            put(self.dousing, dousing, torch.uint8)
+        if position is not None:
+            put(self.pos, position, torch.int32)
+        if altitude is not None:
+            alt = altitude if dev.is_device_tensor(altitude) else torch.as_tensor(np.asarray(altitude, np.float64),
+                                                                                 device=self.device)
+            call("gca_alex_slope_from_altitude", dev.ptr(alt.contiguous()), dev.ptr(self.p_slope), None, E, H, W, st)
+        call("gca_count_cells", dev.ptr(self.grid[self.cur]), E, H, W, self._empty, self._tree, self._fire,
+             dev.ptr(self.counts), st)
+
+    # ------------------------------------------------------------------ step
+    def _obs(self):
+        ctx = {"per_env_context": {"wind_index": self.wind_index, "fire_age": self.age[self.cur],
+                                   "dousing_count": self.dousing, "vegetation": self.vegetation,
+                                   "density": self.density, "time_step": self.time_step, "is_night": self.is_night,
+                                   "true_grid": self.grid[self.cur], "rng_step": self.rng_step},
+               "position": self.pos, "time": self.accu}
+        return self.grid[self.cur], ctx
+
+    def _info(self):
+        return {"reward": self.reward, "terminated": self.done.bool(), "steps_elapsed": self.steps_elapsed,
+                "reward_accumulated": self.reward_accumulated}
+
+    def ca_step(self):
+        """The CA step alone (RepeatCAJax's one step) for every env; swaps the ping-pong buffers."""
+        E, H, W = self.num_envs, self.nrows, self.ncols
+        a, b = self.cur, 1 - self.cur
+        call("gca_alex_step", self.alex_params, E, H, W, dev.ptr(self.grid[a]), dev.ptr(self.grid[b]),
+             dev.ptr(self.age[a]), dev.ptr(self.age[b]), dev.ptr(self.vegetation), dev.ptr(self.density),
+             dev.ptr(self.dousing), dev.ptr(self.p_slope), dev.ptr(self.wind_index), dev.ptr(self.rng_step),
+             None, None, None, None, dev.ptr(self.counts), dev.stream_ptr(self.device))
+        self.cur = b
+
+    def step(self, action):
+        """action: (E, 2) or (E, 3) ints (move, shoot[, extension]); device tensor or numpy."""
+        import torch
+
+        E, H, W = self.num_envs, self.nrows, self.ncols
+        a = action if dev.is_device_tensor(action) else torch.as_tensor(np.asarray(action), device=self.device)
+        a = a.to(torch.int32).reshape(E, -1)[:, :2].contiguous()
+        self.ca_step()
+        call("gca_advenv_post", self.env_params, dev.ptr(a), dev.ptr(self.pos), dev.ptr(self.accu),
+             dev.ptr(self.wind_index), dev.ptr(self.time_step), dev.ptr(self.is_night), dev.ptr(self.dousing), H, W,
+             dev.ptr(self.counts), dev.ptr(self.rng_step), dev.ptr(self.reward), dev.ptr(self.done), E,
+             dev.stream_ptr(self.device))
+        self.steps_elapsed += 1
+        self.reward_accumulated += self.reward
+        terminated = self.done.bool()
+        return self._obs(), self.reward, terminated, torch.zeros_like(terminated), self._info()
+
+    stateless_step = step
+
+    def conditional_reset(self):
+        """Re-inject the initial state of terminated envs (:422-518); time_step/is_night are kept."""
+        import torch
+
+        E, H, W = self.num_envs, self.nrows, self.ncols
+        init = self._initial
+        done = self.done.clone()
+        mask = done.bool()
+        self.steps_elapsed.masked_fill_(mask, 0)
+        self.reward_accumulated.masked_fill_(mask, 0.0)
+        self.rng_step.masked_fill_(mask, 0)  # the reference re-injects the initial JAX key
+        self.counts.copy_(torch.where(mask[:, None], init["counts"], self.counts))
+        t, f = self.counts[:, 1].float(), self.counts[:, 2].float()
+        self.reward.copy_(torch.where(mask, -(f / (t + f + 1e-8)), self.reward))
+        call("gca_reset_where", dev.ptr(self.done), E, H, W, dev.ptr(self.grid[self.cur]), dev.ptr(init["grid"]),
+             dev.ptr(self.age[self.cur]), dev.ptr(init["age"]), dev.ptr(self.dousing), None, dev.ptr(self.pos),
+             dev.ptr(init["pos"]), dev.ptr(self.accu), dev.ptr(self.wind_index), dev.ptr(init["wind_index"]),
+             dev.stream_ptr(self.device))
+        return self._obs(), self.reward, self.done.bool(), torch.zeros_like(mask), self._info()

@@ -1,0 +1,154 @@
+"""BatchedForestFireBulldozerEnv — E ForestFireBulldozer envs resident in HBM.
+
+The batched form of bulldozer.py's MDP (reference bulldozer.py:378-400 +
+ca_env.py:27-62), one env per lane of the env kernels and one strip of rows per
+wave of the CA kernel:
+
+    gca_bulldozer_pre        RepeatCA time bookkeeping (repeat_ca.py:32-45), dir mask (ca_windy.py:53-77)
+    gca_windy_step  x P      the CA passes (P = max repeats any action can trigger)
+    gca_bulldozer_interpass  between passes (parity flip + next roll)
+    gca_bulldozer_post       Move/Modify (move_modify.py:128-134), reward/done (bulldozer.py:180-216)
+
+Grids live in two buffers; env e's current grid is buf[parity[e]][e], so envs whose
+RepeatCA yields 0 repeats this step (most of them: ~1 CA step per 13 env steps at
+256^2 with random actions) move no bytes at all. Cell counts are
+fused into the CA kernel and patched by Modify, so reward/done are O(1) per env.
+"""
+import math
+
+import numpy as np
+
+from ... import _device as dev
+from ..._lib import call
+from ..operators.move_modify import make_params
+from .bulldozer import ACTION_SETS, DEFAULT_WIND, bulldozer_timings, parse_wind
+
+
+class BatchedForestFireBulldozerEnv:
+    def __init__(self, num_envs, nrows, ncols, device=None, seed=0, env_offset=0, speed_move=0.12, speed_act=0.03,
+                 t_move=None, t_shoot=None, t_any=0.001, p_tree=0.90, p_empty=0.10, wind=DEFAULT_WIND,
+                 materialize_obs=True):
+        import torch
+
+        self.device = dev.require_device(device)
+        self.num_envs, self.nrows, self.ncols = E, H, W = int(num_envs), int(nrows), int(ncols)
+        self.seed_value = int(seed)
+        self.env_offset = int(env_offset)
+        self.materialize_obs = materialize_obs
+        self._empty, self._tree, self._fire = 0, 3, 25
+        self._p_tree, self._p_empty = p_tree, p_empty
+        t_act_move, t_act_shoot = bulldozer_timings(H, W, speed_move, speed_act, t_move, t_shoot, t_any)
+        self.t_act_move, self.t_act_shoot, self.t_any = t_act_move, t_act_shoot, t_any
+        p = make_params(ACTION_SETS, {self._tree: self._empty})
+        for a in range(9):
+            p.t_move[a] = 0.0 if a == 4 else t_act_move  # not_move costs _t_act_none (bulldozer.py:285)
+        p.t_shoot[0], p.t_shoot[1] = 0.0, t_act_shoot
+        p.t_any = t_any
+        p.seed = self.seed_value & (2**64 - 1)
+        p.env_offset = self.env_offset
+        p.empty, p.tree, p.fire = self._empty, self._tree, self._fire
+        self.params = p
+        max_t = max(p.t_move[a] for a in range(9)) + max(p.t_shoot[0], p.t_shoot[1]) + t_any
+        self.max_passes = int(math.floor(1.0 + max_t))  # accu < 1 before the step
+        kw = dict(device=self.device)
+        self.buf = torch.zeros((2, E, H, W), dtype=torch.uint8, **kw)
+        self.parity = torch.zeros(E, dtype=torch.uint8, **kw)
+        self.accu = torch.zeros(E, dtype=torch.float64, **kw)
+        self.steps = torch.zeros(E, dtype=torch.int32, **kw)
+        self.dir_mask = torch.zeros(E, dtype=torch.uint8, **kw)
+        self.counts = torch.zeros((E, 3), dtype=torch.int32, **kw)
+        self.pos = torch.zeros((E, 2), dtype=torch.int32, **kw)
+        self.rng_step = torch.zeros(E, dtype=torch.int32, **kw)  # uint32 bits
+        self.done = torch.zeros(E, dtype=torch.uint8, **kw)
+        self.hit = torch.zeros(E, dtype=torch.uint8, **kw)
+        self.reward = torch.zeros(E, dtype=torch.float64, **kw)
+        w = parse_wind(wind) if isinstance(wind, dict) else np.asarray(wind, dtype=np.float64)
+        self.wind = dev.to_device(np.broadcast_to(w.reshape(-1, 9), (E, 9)), torch.float64, self.device)
+        self.steps_elapsed = torch.zeros(E, dtype=torch.int64, **kw)
+
+    # ------------------------------------------------------------------ state
+    def grids(self):
+        """(E, H, W) uint8 view of every env's current grid (one gather pass)."""
+        import torch
+
+        return torch.where(self.parity.bool()[:, None, None], self.buf[1], self.buf[0])
+
+    def reset(self, seed=None, grids=None, positions=None):
+        """Reset all envs. Initial distribution of bulldozer.py:233-275, drawn with Philox
+        (grid) and a numpy Generator seeded from `seed` (fire / bulldozer noise)."""
+        import torch
+
+        E, H, W = self.num_envs, self.nrows, self.ncols
+        st = dev.stream_ptr(self.device)
+        rng = np.random.default_rng(self.seed_value if seed is None else seed)
+        if grids is not None:
+            self.buf[0].copy_(dev.to_device(np.asarray(grids).reshape(E, H, W).astype(np.uint8), torch.uint8,
+                                            self.device))
+        else:
+            cdf = torch.tensor([self._p_empty, self._p_empty + self._p_tree, 1.0], dtype=torch.float32,
+                               device=self.device)
+            vals = torch.tensor([self._empty, self._tree, self._fire], dtype=torch.uint8, device=self.device)
+            call("gca_fill_categorical", dev.ptr(self.buf[0]), H * W, E, self.env_offset,
+                 (self.seed_value if seed is None else int(seed)) & (2**64 - 1), dev.ptr(cdf), dev.ptr(vals), 3, st)
+            # one FIRE around the lower-left quadrant, noise in [0, N/12) (bulldozer.py:221-253)
+            fr = 3 * H // 4 + rng.integers(0, max(1, int(H / 12)), E)
+            fc = W // 4 + rng.integers(0, max(1, int(W / 12)), E)
+            idx = torch.arange(E, device=self.device)
+            self.buf[0][idx, torch.as_tensor(fr, device=self.device), torch.as_tensor(fc, device=self.device)] = \
+                self._fire
+        if positions is not None:
+            pos = np.asarray(positions).reshape(E, 2)
+        else:
+            pos = np.stack([H // 4 + rng.integers(0, max(1, int(H / 12)), E),
+                            3 * W // 4 + rng.integers(0, max(1, int(W / 12)), E)], axis=1)
+        self.pos.copy_(torch.as_tensor(pos.astype(np.int32), device=self.device))
+        self.parity.zero_()
+        self.accu.zero_()
+        self.done.zero_()
+        self.hit.zero_()
+        self.rng_step.zero_()
+        self.steps_elapsed.zero_()
+        call("gca_count_cells", dev.ptr(self.buf[0]), E, H, W, self._empty, self._tree, self._fire,
+             dev.ptr(self.counts), st)
+        return self._obs(), {"hit": self.hit}
+
+    def _obs(self):
+        ctx = {"wind": self.wind, "position": self.pos, "time": self.accu}
+        return (self.grids() if self.materialize_obs else None), ctx
+
+    # ------------------------------------------------------------------ step
+    def step(self, action):
+        """action: (E, 2) int (move in [0,9), shoot in {0,1}); device tensor or numpy."""
+        import torch
+
+        E, H, W = self.num_envs, self.nrows, self.ncols
+        a = action if dev.is_device_tensor(action) else torch.as_tensor(np.asarray(action), device=self.device)
+        a = a.to(torch.int32).reshape(E, 2).contiguous()
+        st = dev.stream_ptr(self.device)
+        p = self.params
+        call("gca_bulldozer_pre", p, dev.ptr(a), dev.ptr(self.accu), dev.ptr(self.steps), dev.ptr(self.done),
+             dev.ptr(self.wind), 9, dev.ptr(self.rng_step), dev.ptr(self.dir_mask), dev.ptr(self.counts), E, st)
+        P = self.max_passes
+        for pss in range(P):
+            call("gca_windy_step", dev.ptr(self.buf[0]), dev.ptr(self.buf[1]), dev.ptr(self.parity),
+                 dev.ptr(self.steps), pss, dev.ptr(self.dir_mask), E, H, W, self._empty, self._tree, self._fire, 0,
+                 dev.ptr(self.counts), st)
+            if pss < P - 1:
+                call("gca_bulldozer_interpass", p, pss, dev.ptr(self.steps), dev.ptr(self.parity),
+                     dev.ptr(self.wind), 9, dev.ptr(self.rng_step), dev.ptr(self.dir_mask), E, st)
+        call("gca_bulldozer_post", p, P - 1, dev.ptr(a), dev.ptr(self.steps), dev.ptr(self.parity),
+             dev.ptr(self.buf[0]), dev.ptr(self.buf[1]), H, W, dev.ptr(self.pos), dev.ptr(self.counts),
+             dev.ptr(self.rng_step), dev.ptr(self.done), dev.ptr(self.hit), dev.ptr(self.reward), E, st)
+        self.steps_elapsed += (self.steps >= 0).to(torch.int64)
+        terminated = self.done.bool()
+        truncated = torch.zeros_like(terminated)
+        return self._obs(), self.reward, terminated, truncated, {"hit": self.hit, "ca_steps": self.steps}
+
+    def ca_step_all(self, dir_mask=None):
+        """One forced WindyForestFire step of every env (bench 'CA-only' mode, steps[E] = 1)."""
+        E, H, W = self.num_envs, self.nrows, self.ncols
+        st = dev.stream_ptr(self.device)
+        call("gca_windy_step", dev.ptr(self.buf[0]), dev.ptr(self.buf[1]), dev.ptr(self.parity), None, 0,
+             dev.ptr(self.dir_mask if dir_mask is None else dir_mask), E, H, W, self._empty, self._tree, self._fire,
+             0, None, st)
+        self.parity ^= 1

@@ -1,0 +1,138 @@
+"""ForestFireHelicopterEnv — drop-in for the reference env (helicopter.py:20-236).
+
+The Drossel–Schwabl CA (gca_ds_step), Move/Modify (gca_move_modify) and the reward
+cell counts (gca_count_cells) run on the GPU; the freeze countdown is host logic.
+"""
+from typing import Optional
+
+import numpy as np
+
+from ... import _device as dev
+from ..._config import TYPE_BOX, TYPE_INT
+from ..._lib import call
+from ...ca_env import CAEnv
+from ...grid_space import GridSpace
+from ...operator import Operator
+from ...spaces import Box, Discrete, MultiDiscrete
+from ...spaces import Tuple as TupleSpace
+from ..operators import ForestFire, Modify, Move, MoveModify
+
+
+class ForestFireHelicopterEnv(CAEnv):
+    metadata = {"render_modes": ["human"]}
+
+    @property
+    def MDP(self):
+        return self._MDP
+
+    @property
+    def initial_state(self):
+        if self._resample_initial:
+            self.grid = self.grid_space.sample()
+            ca_params = np.array([self._p_fire, self._p_tree], dtype=TYPE_BOX)
+            pos = np.array([self.nrows // 2, self.ncols // 2])
+            freeze = np.array(self._max_freeze)
+            self.context = ca_params, pos, freeze
+            self._initial_state = self.grid, self.context
+        self._resample_initial = False
+        return self._initial_state
+
+    def __init__(self, nrows, ncols, speed: float = 0.5, freeze: Optional[int] = None, **kwargs):
+        super().__init__(nrows, ncols, **kwargs)
+        self.title = "ForestFireHelicopter" + str(nrows) + "x" + str(ncols)
+        self._n_actions = 9
+        self._reward_per_empty, self._reward_per_tree, self._reward_per_fire = 0.0, 1.0, -1.0
+        self._empty, self._tree, self._fire = 0, 1, 2
+        self._p_fire, self._p_tree = 0.033, 0.333
+        self._effects = {self._fire: self._empty}
+        scale = (nrows + ncols) // 2
+        self._max_freeze = int(speed * scale) if freeze is None else freeze
+        self._action_sets = {"up": {0, 1, 2}, "down": {6, 7, 8}, "left": {0, 3, 6}, "right": {2, 5, 8},
+                             "not_move": {4}}
+        self._set_spaces()
+        self.cellular_automaton = ForestFire(self._empty, self._tree, self._fire, **self.ca_space)
+        self.move = Move(self._action_sets, **self.move_space)
+        self.modify = Modify(self._effects, **self.modify_space)
+        self.move_modify = MoveModify(self.move, self.modify, **self.move_modify_space)
+        self._MDP = MDP(self.cellular_automaton, self.move_modify, self._max_freeze, **self.MDP_space)
+
+    def render(self, mode="human"):
+        return None
+
+    def count_cells(self, grid=None):
+        import torch
+        from collections import Counter
+
+        grid = self.grid if grid is None else grid
+        device = dev.require_device()
+        g = dev.to_device(np.asarray(grid).astype(np.uint8), torch.uint8, device)
+        counts = torch.empty(3, dtype=torch.int32, device=device)
+        call("gca_count_cells", dev.ptr(g), 1, self.nrows, self.ncols, self._empty, self._tree, self._fire,
+             dev.ptr(counts), dev.stream_ptr(device))
+        c = counts.cpu().numpy().tolist()
+        return Counter({v: n for v, n in zip((self._empty, self._tree, self._fire), c) if n})
+
+    def _award(self):
+        """helicopter.py:120-135."""
+        ncells = self.nrows * self.ncols
+        dict_counts = self.count_cells(self.grid)
+        cell_counts = np.array([dict_counts[self._empty], dict_counts[self._tree], dict_counts[self._fire]])
+        cell_counts_relative = cell_counts / ncells
+        reward_weights = np.array([self._reward_per_empty, self._reward_per_tree, self._reward_per_fire])
+        return np.dot(reward_weights, cell_counts_relative)
+
+    def _is_done(self):
+        return False
+
+    def _report(self):
+        return {"hit": self.modify.hit}
+
+    def _set_spaces(self):
+        self.ca_params_space = Box(0.0, 1.0, shape=(2,), dtype=TYPE_BOX)
+        self.position_space = MultiDiscrete([self.nrows, self.ncols], dtype=TYPE_INT)
+        self.freeze_space = Discrete(self._max_freeze + 1)
+        self.context_space = TupleSpace((self.ca_params_space, self.position_space, self.freeze_space))
+        self.grid_space = GridSpace(values=[self._empty, self._tree, self._fire], shape=(self.nrows, self.ncols),
+                                    dtype=TYPE_INT)
+        self.action_space = Discrete(self._n_actions)
+        self.observation_space = TupleSpace((self.grid_space, self.context_space))
+        self.ca_space = {"grid_space": self.grid_space, "action_space": self.action_space,
+                         "context_space": self.ca_params_space}
+        self.move_space = {"grid_space": self.grid_space, "action_space": self.action_space,
+                           "context_space": self.position_space}
+        self.modify_space = {"grid_space": self.grid_space, "action_space": Discrete(2),
+                             "context_space": self.position_space}
+        self.move_modify_space = {"grid_space": self.grid_space,
+                                  "action_space": TupleSpace((self.action_space, Discrete(2))),
+                                  "context_space": self.position_space}
+        self.MDP_space = {"grid_space": self.grid_space, "action_space": self.action_space,
+                          "context_space": self.context_space}
+
+
+class MDP(Operator):
+    """helicopter.py:198-236: CA every max_freeze+1 steps, MoveModify always."""
+
+    grid_dependant = True
+    action_dependant = True
+    context_dependant = True
+
+    deterministic = False
+
+    def __init__(self, cellular_automaton, move_modify, max_freeze, *args, **kwargs):
+        super().__init__(*args, **kwargs)
+        self.move_modify = move_modify
+        self.ca = cellular_automaton
+        self.suboperators = (cellular_automaton, move_modify)
+        self.max_freeze = max_freeze
+        self.freeze_space = Discrete(max_freeze + 1)
+
+    def update(self, grid, action, context):
+        ca_params, position, freeze = context
+        if freeze == 0:
+            grid, ca_params = self.ca(grid, None, ca_params)
+            grid, position = self.move_modify(grid, (action, True), position)
+            freeze = np.array(self.max_freeze)
+        else:
+            grid, position = self.move_modify(grid, (action, True), position)
+            freeze = np.array(freeze - 1)
+        return grid, (ca_params, position, freeze)

@@ -1,0 +1,12 @@
+"""GPU operators with the reference's names (forest_fire/operators/__init__.py:1-20)."""
+from .ca_alexandridis import PartiallyObservableForestFireJax
+from .ca_DrosselSchwabl import ForestFire
+from .ca_windy import WindyForestFire
+from .move_modify import Modify, Move, MoveModify
+from .repeat_ca import RepeatCA
+
+# The JAX-suffixed operators of the reference are served by the same classes.
+MoveJax, ModifyJax, MoveModifyJax, RepeatCAJax = Move, Modify, MoveModify, RepeatCA
+
+__all__ = ["WindyForestFire", "PartiallyObservableForestFireJax", "ForestFire", "Move", "Modify", "MoveModify",
+           "RepeatCA", "MoveJax", "ModifyJax", "MoveModifyJax", "RepeatCAJax"]

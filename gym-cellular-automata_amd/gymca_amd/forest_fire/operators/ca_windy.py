@@ -1,0 +1,120 @@
+"""WindyForestFire on the GPU — drop-in for the reference operator (ca_windy.py:11-173).
+
+Same constructor (empty, tree, fire, spaces), same class flags, same
+`update(grid, action, wind) -> (new_grid, wind)`. The CA step runs in
+libgca_hip.so (gca_windy_dirmask + gca_windy_step); nothing is computed on the host.
+
+Differences, all documented in DESIGN.md:
+  * the 3x3 uniform roll (ca_windy.py:57-60, an unseeded Box sample in the
+    reference) comes from Philox(self.philox_seed, call counter) on the device; an
+    explicit roll can be injected with `update(..., roll=R)` or queued in
+    `self.roll_queue` (golden-vector parity);
+  * `wind` may be the bulldozer env's {"wind": W} context: it is
+    unwrapped, and returned unchanged;
+  * `grid` may be a numpy array (H, W) / (E, H, W) — returned as numpy of the same
+    dtype — or a device uint8 tensor (returned on the device). A stack of E grids gets
+    one independent roll per grid.
+"""
+from collections import namedtuple
+
+import numpy as np
+
+from ... import _device as dev
+from ..._config import TYPE_BOX
+from ..._lib import call
+from ...operator import Operator
+from ...spaces import Box
+
+Breaks = namedtuple("Breaks", ["keep", "propagate", "consume"])
+
+
+class WindyForestFire(Operator):
+    grid_dependant = True
+    action_dependant = False
+    context_dependant = True
+
+    deterministic = False
+
+    _identity = 2**11
+    _propagation = 2**3
+
+    _row_k = 3
+    _col_k = 3
+
+    def __init__(self, empty=0, tree=3, fire=25, *args, **kwargs):
+        super().__init__(*args, **kwargs)
+        self._empty = empty
+        self._tree = tree
+        self._fire = fire
+        self._assert_correctness()
+        dev.check_u8_codes((empty, tree, fire))
+        self.breaks = self._get_breaks()
+        if self.context_space is None:
+            self.context_space = Box(0.0, 1.0, shape=(3, 3), dtype=TYPE_BOX)
+        self._calls = 0
+        self.roll_queue = []  # rolls injected in FIFO order (golden-vector replay of env episodes)
+
+    # ------------------------------------------------------------------ API
+    def update(self, grid, action, wind, *, roll=None):
+        w = wind["wind"] if isinstance(wind, dict) else wind
+        device = dev.require_device()
+        on_device = dev.is_device_tensor(grid)
+        g = grid if on_device else np.asarray(grid)
+        shape = tuple(g.shape)
+        if len(shape) not in (2, 3):
+            raise ValueError("grid must be (H, W) or (E, H, W)")
+        E = 1 if len(shape) == 2 else shape[0]
+        H, W = shape[-2:]
+
+        import torch
+
+        if on_device:
+            src = g.to(torch.uint8).reshape(E, H, W).contiguous()
+            exact = 0
+        else:
+            values = np.unique(g)
+            exact = 0 if set(values.tolist()) <= {self._empty, self._tree, self._fire} else 1
+            if values.size and (values.min() < 0 or values.max() > 255):
+                raise ValueError("cell values must fit the u8 device layout (0..255)")
+            src = dev.to_device(g.reshape(E, H, W).astype(np.uint8), torch.uint8, device)
+        dst = torch.empty_like(src)
+        wind_d = dev.to_device(np.broadcast_to(np.asarray(w, dtype=np.float64), (E, 3, 3)), torch.float64, device)
+        roll_d = None
+        if roll is None and self.roll_queue:
+            roll = self.roll_queue.pop(0)
+        if roll is not None:
+            roll_d = dev.to_device(np.broadcast_to(np.asarray(roll, dtype=np.float64), (E, 3, 3)), torch.float64, device)
+        step = torch.full((E,), self._calls, dtype=torch.int32, device=device)
+        mask = torch.empty(E, dtype=torch.uint8, device=device)
+        st = dev.stream_ptr(device)
+        call("gca_windy_dirmask", dev.ptr(wind_d), 9, dev.ptr(roll_d), self.philox_seed & (2**64 - 1),
+             dev.ptr(step), None, 0, 0, dev.ptr(mask), E, st)
+        call("gca_windy_step", dev.ptr(src), dev.ptr(dst), None, None, 0, dev.ptr(mask), E, H, W,
+             self._empty, self._tree, self._fire, exact, None, st)
+        self._calls += 1
+        if on_device:
+            return dst.reshape(shape), wind
+        out = dst.cpu().numpy().reshape(shape)
+        return out.astype(np.asarray(grid).dtype, copy=False), wind
+
+    # ------------------------------------------------------- reference helpers
+    def _get_breaks(self):
+        """3 breaks for 4 rules (ca_windy.py:84-100)."""
+        keep_break = self._identity * self._tree
+        propagate_break = self._identity * self._tree + self._propagation * self._fire
+        consume_break = self._identity * self._fire
+        return Breaks(keep_break, propagate_break, consume_break)
+
+    def _assert_correctness(self):
+        """Constructor invariants of the reference (ca_windy.py:141-173)."""
+        assert self._row_k == 3, "Only Moore's neighborhood"
+        assert self._col_k == 3, "Only Moore's neighborhood"
+        n = 8
+        i, p = self._identity, self._propagation
+        E, T, F = self._empty, self._tree, self._fire
+        assert E < T and T < F
+        assert p < i
+        worst = n * p * F
+        assert i * E + worst < i * T, "Dead / Keep"
+        assert i * T + n * p * T < i * T + p * F, "Keep / Propagate"
+        assert i * T + worst < i * F, "Propagate / Consume"

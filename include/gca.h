@@ -1,0 +1,209 @@
+/*
+ * gca.h — C-ABI of libgca_hip.so, the MI355X (gfx950) forest-fire CA hot path.
+ *
+ * Boundary contract:
+ *   - plain extern "C", int status (GCA_OK = 0), gca_last_error() for the message;
+ *   - every array argument is a DEVICE pointer owned by the caller (e.g. a torch
+ *     tensor's data_ptr()); parameter structs are HOST pointers read at call time;
+ *   - `stream` is a hipStream_t (NULL = legacy default stream); calls only enqueue
+ *     work: no allocation, no synchronisation, so they can be captured in a hipGraph;
+ *   - one caller per stream (thread-compatible, not thread-safe).
+ *
+ * Cell grids are u8, laid out (env, row, col) row-major. Cell codes are the
+ * reference's integer values (ForestFireBulldozer EMPTY=0 TREE=3 FIRE=25,
+ * Advanced/Helicopter 0/1/2); the host side checks they fit in u8.
+ *
+ * RNG: counter-based Philox4x32-10 (Random123), key = (seed lo, seed hi),
+ * counter = (slot, global env id, per-env step, stream tag). See DESIGN.md §RNG.
+ */
+#ifndef GCA_H
+#define GCA_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GCA_OK 0
+#define GCA_ERR_ARG 1
+#define GCA_ERR_HIP 2
+#define GCA_ERR_UNSUPPORTED 3
+
+#define GCA_MAX_RADIUS 8     /* heat-kernel radius ceil(log2 N)-2 <= 8  <=>  N <= 1024 */
+
+/* Philox stream tags (counter word 3). */
+#define GCA_TAG_WINDY_ROLL 0x574E4459u /* 'WNDY' : 3x3 roll of WindyForestFire      */
+#define GCA_TAG_ALEX_CELL  0x414C5843u /* 'ALXC' : per-cell draws of Alexandridis    */
+#define GCA_TAG_ALEX_WIND  0x414C5857u /* 'ALXW' : per-env wind change               */
+#define GCA_TAG_ACTION     0x41435449u /* 'ACTI' : synthetic actions (bench)          */
+#define GCA_TAG_INIT       0x494E4954u /* 'INIT' : synthetic initial states           */
+#define GCA_TAG_DS_CELL    0x44534345u /* 'DSCE' : Drossel-Schwabl per-cell draws     */
+
+/* ------------------------------------------------------------------ generic */
+
+const char* gca_last_error(void);
+int gca_version(void);
+
+/* Philox4x32-10 over n counters (ctr[n][4] device, out[n][4] device). KAT hook. */
+int gca_philox(const uint32_t* ctr, uint32_t key0, uint32_t key1, uint32_t* out, int64_t n, void* stream);
+
+/* counts[e][0..2] = #cells == v0/v1/v2 in grid e (overwrites). ca_env.py:94-99 count_cells. */
+int gca_count_cells(const uint8_t* grid, int E, int H, int W, int v0, int v1, int v2, int32_t* counts, void* stream);
+
+/* ------------------------------------------------------- WindyForestFire ---
+ * Replaces WindyForestFire._get_failed_propagations_mask + _get_kernel
+ * (ca_windy.py:53-77): dir_mask[e] bit d (d = 3x3 index row-major, centre
+ * skipped) is set iff roll[d] < wind[d]  (the reference keeps d iff NOT wind<=roll).
+ * wind: [E][9] f64 with env stride wind_stride (0 = one wind shared by all envs).
+ * roll: [E][9] f64 injected uniforms, or NULL -> Philox(seed, (d/2, env_offset+e,
+ *       rng_step[e] + pass, GCA_TAG_WINDY_ROLL)), 53-bit doubles.
+ * Only envs with steps == NULL || steps[e] > pass are written.                */
+int gca_windy_dirmask(const double* wind, int64_t wind_stride, const double* roll, uint64_t seed,
+                      const uint32_t* rng_step, const int32_t* steps, int pass, int env_offset,
+                      uint8_t* dir_mask, int E, void* stream);
+
+/* One WindyForestFire CA step (ca_windy.py:41-51, scipy convolve2d mode="same",
+ * fill=empty, then the 3 thresholds of _translate_analogic_to_discrete :102-139).
+ * Env e participates iff steps == NULL || steps[e] > pass; it reads
+ * buf[parity ? parity[e] : 0] and writes the other buffer (parity is NOT flipped here).
+ * force_exact = 1 selects the literal threshold kernel; 0 lets the library use the
+ * SWAR kernel when it is exact (empty == 0, all cells in {empty, tree, fire}: the
+ * caller guarantees the latter; W = 16*2^j <= 1024, 16-B aligned buffers).
+ * counts (nullable, [E][3] empty/tree/fire of the NEW grid) are ACCUMULATED with
+ * atomics: the caller zeroes the participating rows first.                    */
+int gca_windy_step(uint8_t* buf0, uint8_t* buf1, const uint8_t* parity, const int32_t* steps, int pass,
+                   const uint8_t* dir_mask, int E, int H, int W, int empty, int tree, int fire,
+                   int force_exact, int32_t* counts, void* stream);
+
+/* --------------------------------------------- ForestFireBulldozer (batched)
+ * bulldozer.py:393-400 MDP = RepeatCA (repeat_ca.py:32-45) then MoveModify
+ * (move_modify.py:128-134); reward/done bulldozer.py:180-216.                 */
+typedef struct {
+    double t_move[9];        /* _movement_timings (bulldozer.py:277-286)      */
+    double t_shoot[2];       /* _shooting_timings                              */
+    double t_any;            /* time_per_state (bulldozer.py:297)              */
+    uint64_t seed;           /* Philox key for the windy roll                  */
+    int32_t env_offset;      /* global id of env 0 of this shard               */
+    int32_t empty, tree, fire;
+    int32_t up_mask, down_mask, left_mask, right_mask; /* action sets as bitmasks over 0..8 */
+    int16_t effect[256];     /* Modify effects: new value, or -1 if not a key  */
+} gca_bulldozer_params;
+
+/* Before the CA passes: for live envs (done[e]==0) accu += (t_move[a0]+t_shoot[a1]) + t_any,
+ * (accu, steps) = modf(accu); zero counts of stepping envs; dir_mask for pass 0.
+ * Done envs get steps = 0.                                                      */
+int gca_bulldozer_pre(const gca_bulldozer_params* p, const int32_t* action, double* accu, int32_t* steps,
+                      const uint8_t* done, const double* wind, int64_t wind_stride, const uint32_t* rng_step,
+                      uint8_t* dir_mask, int32_t* counts, int E, void* stream);
+/* Between CA passes `pass` and `pass+1`: flip parity of envs that stepped in `pass`
+ * and draw the dir_mask for pass+1.                                             */
+int gca_bulldozer_interpass(const gca_bulldozer_params* p, int pass, const int32_t* steps, uint8_t* parity,
+                            const double* wind, int64_t wind_stride, const uint32_t* rng_step, uint8_t* dir_mask,
+                            int E, void* stream);
+/* After the last pass (index last_pass): flip parity, Move, Modify (in place on the
+ * current buffer), adjust counts, reward = -(f/(t+f)) (NaN if t+f==0), done = (f==0),
+ * rng_step += steps. Done-on-entry envs: reward 0, nothing moves.                  */
+int gca_bulldozer_post(const gca_bulldozer_params* p, int last_pass, const int32_t* action, const int32_t* steps,
+                       uint8_t* parity, uint8_t* buf0, uint8_t* buf1, int H, int W, int32_t* pos,
+                       int32_t* counts, uint32_t* rng_step, uint8_t* done, uint8_t* hit, double* reward,
+                       int E, void* stream);
+
+/* Move then Modify for E envs (move_modify.py:37-134): action[e] = (move, shoot);
+ * uses p->up/down/left/right_mask and p->effect; grid may be NULL (Move only); hit nullable. */
+int gca_move_modify(const gca_bulldozer_params* p, const int32_t* action, int32_t* pos, uint8_t* grid, int H, int W,
+                    uint8_t* hit, int E, void* stream);
+
+/* -------------------------------------------- Alexandridis (advanced env CA) */
+typedef struct {
+    int32_t R;                 /* burn_kernel_radius (ca_alexandridis_jax.py:62)              */
+    float heat_dw[GCA_MAX_RADIUS + 1]; /* w_k - w_{k+1} (f32), w_k = heat weight at Chebyshev distance k (k=0 centre, w_{R+1}=0), :108-153 */
+    float dous_inner, dous_border;    /* 5x5 dousing weights :64-105                          */
+    float veg1p[6], den1p[6];  /* 1 + veg_probs / den_probs, f32 (:170-184, clip 1..5)        */
+    float p_tree;              /* shared_context["p_tree"] (:386)                              */
+    int32_t age_lo, age_hi;    /* randint(fire_age_min, fire_age_max) bounds, truncated (:368) */
+    uint64_t seed;
+    int32_t env_offset;
+    int32_t empty, tree, fire; /* 0, 1, 2 in AdvancedForestFireBulldozerEnv                  */
+    int32_t n_winds;
+    float winds[16][9];        /* shared_context["winds"][i][0] wind matrices (row-major 3x3)  */
+} gca_alex_params;
+
+/* p_slope[e][d][r][c] = exp_f32(0.078f * slope[e][r][c][d']) for the 8 non-centre d'
+ * (ca_alexandridis_jax.py:199-200). exp_f32 is the deterministic expf of DESIGN.md. */
+int gca_alex_prepare_slope(const float* slope, float* p_slope, int E, int H, int W, void* stream);
+
+/* One CA step of PartiallyObservableForestFireJax._update_grid (ca_alexandridis_jax.py:321-424).
+ * grid u8, fire_age i16, vegetation/density/dousing u8 (E,H,W); p_slope (E,8,H,W) f32.
+ * Draws: inj_burn [E][H][W][9] f32, inj_grow [E][H][W] f32, inj_age [E][H][W] i32 (all three
+ *        given = injected mode, the reference rule verbatim), or all NULL = Philox mode
+ *        (one Philox4x32-10 block per cell, burn test against 1 - prod(1 - clamp01(p_d))).
+ * prob_out (nullable, debug) [E][H][W][8] f32 burn probabilities of every cell.
+ * counts (nullable) [E][3] of the NEW grid, OVERWRITTEN (memset inside).          */
+int gca_alex_step(const gca_alex_params* p, int E, int H, int W, const uint8_t* grid_in, uint8_t* grid_out,
+                  const int16_t* age_in, int16_t* age_out, const uint8_t* veg, const uint8_t* den,
+                  const uint8_t* dousing, const float* p_slope, const int32_t* wind_index, const uint32_t* rng_step,
+                  const float* inj_burn, const float* inj_grow, const int32_t* inj_age, float* prob_out,
+                  int32_t* counts, void* stream);
+
+/* Wind change of PartiallyObservableForestFireJax.update (ca_alexandridis_jax.py:442-451) for E envs:
+ * u < p_wind_change -> wind_index = (wind_index + k) % n_winds, k in [1, 8).
+ * inj_u/inj_k injected draws, or both NULL -> Philox((0, env_offset+e, rng_step[e], ALXW)) words 0/1. */
+int gca_alex_wind_change(float p_wind_change, int n_winds, uint64_t seed, int env_offset, const uint32_t* rng_step,
+                         const float* inj_u, const int32_t* inj_k, int32_t* wind_index, int E, void* stream);
+
+/* get_slope (init_utils.py:166-200) on the device from altitude [E][H][W] f64 (NULL = flat),
+ * f64 -> f32 like jnp.array, then p_slope as in gca_alex_prepare_slope. slope_out (nullable)
+ * receives the f32 slope [E][H][W][3][3]. */
+int gca_alex_slope_from_altitude(const double* altitude, float* p_slope, float* slope_out, int E, int H, int W,
+                                 void* stream);
+
+/* --------------------------------- AdvancedForestFireBulldozer env step (batched)
+ * advanced_bulldozer.py:1103-1133 minus observations, + _award/_is_done :597-633.  */
+typedef struct {
+    float t_move[9], t_shoot[2], t_any;  /* f32 like the JAX env (all moves cost t_move: :745-760) */
+    float p_wind_change;                 /* 0.06 (:210)                                            */
+    int32_t day_length;                  /* 400 (:733)                                             */
+    uint64_t seed;
+    int32_t env_offset;
+    int32_t n_winds;
+    int32_t up_mask, down_mask, left_mask, right_mask;
+} gca_advenv_params;
+
+/* After gca_alex_step: wind change (repeat: ca_alexandridis_jax.py:442-451), time
+ * accumulation (repeat_ca_jax.py:191-198, f32), MoveJax, ModifyJax (dousing[r][c] = 1
+ * if shoot==1), time_step += 1, is_night toggle, reward = -(f/(t+f+1e-8)) f32,
+ * done = no fire, rng_step += 1.                                                  */
+int gca_advenv_post(const gca_advenv_params* p, const int32_t* action, int32_t* pos, float* accu,
+                    int32_t* wind_index, int32_t* time_step, int32_t* is_night, uint8_t* dousing, int H, int W,
+                    const int32_t* counts, uint32_t* rng_step, float* reward, uint8_t* done, int E, void* stream);
+
+/* conditional_reset (advanced_bulldozer.py:422-518): envs with done[e] copy their
+ * initial grid/age/dousing/position/time/wind_index (and clear done).            */
+int gca_reset_where(const uint8_t* done, int E, int H, int W, uint8_t* grid, const uint8_t* grid0,
+                    int16_t* age, const int16_t* age0, uint8_t* dousing, const uint8_t* dousing0,
+                    int32_t* pos, const int32_t* pos0, float* accu, int32_t* wind_index, const int32_t* wind_index0,
+                    void* stream);
+
+/* Synthetic inputs for benches/tests (Philox, GCA_TAG_INIT / GCA_TAG_ACTION). */
+int gca_fill_categorical(uint8_t* out, int64_t n_per_env, int E, int env_offset, uint64_t seed,
+                         const float* cdf, const uint8_t* values, int n_values, void* stream);
+int gca_random_actions(int32_t* action, int E, int env_offset, uint64_t seed, const uint32_t* rng_step,
+                       void* stream);
+
+/* ------------------------------------------ Drossel-Schwabl (helicopter CA)
+ * ForestFire.update (ca_DrosselSchwabl.py:32-66). The reference draws one f64
+ * uniform per TREE-without-burning-neighbour and per EMPTY cell, in row-major
+ * order, from op.np_random. Exact-stream mode: uniforms[] holds those draws in
+ * order (n = gca_ds_count_draws). One workgroup per env (scan over the grid).   */
+int gca_ds_count_draws(const uint8_t* grid, int E, int H, int W, int empty, int tree, int fire,
+                       int32_t* n_draws, void* stream);
+int gca_ds_step(const uint8_t* grid_in, uint8_t* grid_out, int E, int H, int W, int empty, int tree, int fire,
+                const double* thresholds /*[E][2]: cdf0 of choice([T,F], p=[p_fire,1-p_fire]), same for p_tree*/,
+                const double* uniforms, const int64_t* uniform_offset, uint64_t seed, const uint32_t* rng_step,
+                int env_offset, int32_t* counts, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GCA_H */

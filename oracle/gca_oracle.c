@@ -1,0 +1,226 @@
+/*
+ * gca_oracle.c — plain-C restatement of the Alexandridis step (reference
+ * ca_alexandridis_jax.py:164-206, 321-460) in the exact f32 evaluation order the
+ * device kernel documents, plus Philox4x32-10 and the deterministic exp_f32.
+ * TEST INFRASTRUCTURE ONLY (bit-exact checker of libgca_hip.so and the CPU baseline
+ * of bench.py); it shares no source with the product and is never linked into it.
+ *
+ * Build: oracle/Makefile (gcc -O2 -ffp-contract=off; no -ffast-math).
+ *
+ * Restated algorithm, per cell (r, c) of env e, zero (EMPTY) padding:
+ *   B_k   = #FIRE in the (2k+1)^2 box, D_k = sum of dousing in the box (k = 1, 2)
+ *   heat  = sum_{k=0..R} dw_k * B_k         (dw_k = w_k - w_{k+1}: ring weights, f32)
+ *   dous  = (inner - border) * D_1 + border * D_2
+ *   p_h   = heat - dous                      (:198)
+ *   p_d   = ((((p_h * av) * ad) * wind[d]) * p_slope[d])                       (:206)
+ *   injected: TREE -> FIRE iff exists fire neighbour d with u[d] < p_d (:379-383)
+ *   philox  : TREE -> FIRE iff u0 < 1 - prod_{fire d} (1 - clamp01(p_d))
+ *   EMPTY -> TREE iff u < p_tree; FIRE -> EMPTY iff age <= 1; ages (:394-423).
+ */
+#include <math.h>
+#include <stdlib.h>
+#include <stdint.h>
+#include <string.h>
+
+#define TAG_ALEX_CELL 0x414C5843u
+#define TAG_ALEX_WIND 0x414C5857u
+
+typedef struct {
+    int32_t R;
+    float heat_dw[9];
+    float dous_inner, dous_border;
+    float veg1p[6], den1p[6];
+    float p_tree;
+    int32_t age_lo, age_hi;
+    uint64_t seed;
+    int32_t env_offset;
+    int32_t empty, tree, fire;
+    int32_t n_winds;
+    float winds[16][9];
+} oracle_alex_params;
+
+/* ------------------------------------------------------------------ Philox4x32-10 */
+static void philox(const uint32_t in[4], uint32_t k0, uint32_t k1, uint32_t out[4]) {
+    uint32_t c0 = in[0], c1 = in[1], c2 = in[2], c3 = in[3];
+    for (int i = 0; i < 10; ++i) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0, n1 = (uint32_t)p1;
+        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1, n3 = (uint32_t)p0;
+        c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+void oracle_philox(const uint32_t* ctr, uint32_t k0, uint32_t k1, uint32_t* out, long n) {
+    for (long i = 0; i < n; ++i) philox(ctr + 4 * i, k0, k1, out + 4 * i);
+}
+
+static float u01(uint32_t x) { return (float)(x >> 8) * 0x1.0p-24f; }
+static int32_t randint_ms(uint32_t x, int32_t lo, int32_t hi) {
+    if (hi <= lo) return lo;
+    return lo + (int32_t)(((uint64_t)x * (uint32_t)(hi - lo)) >> 32);
+}
+
+/* ------------------------------------------------------------------ exp_f32 */
+float oracle_exp_f32(float x) {
+    x = fminf(fmaxf(x, -80.0f), 80.0f);
+    const float kf = rintf(x * 1.44269504088896341f);
+    const int k = (int)kf;
+    float r = fmaf(kf, -0.693145751953125f, x);
+    r = fmaf(kf, -1.42860682030941723212e-6f, r);
+    float p = 1.98412698412698413e-4f;
+    p = fmaf(p, r, 1.38888888888888889e-3f);
+    p = fmaf(p, r, 8.33333333333333333e-3f);
+    p = fmaf(p, r, 4.16666666666666667e-2f);
+    p = fmaf(p, r, 1.66666666666666667e-1f);
+    p = fmaf(p, r, 0.5f);
+    p = fmaf(p, r * r, r);
+    p = p + 1.0f;
+    uint32_t bits;
+    memcpy(&bits, &p, 4);
+    bits += (uint32_t)k << 23;
+    float y;
+    memcpy(&y, &bits, 4);
+    return y;
+}
+
+void oracle_alex_prepare_slope(const float* slope, float* p_slope, int E, int H, int W) {
+    const long HW = (long)H * W;
+    for (int e = 0; e < E; ++e)
+        for (long cell = 0; cell < HW; ++cell)
+            for (int d = 0; d < 8; ++d) {
+                const float s = slope[((long)e * HW + cell) * 9 + (d < 4 ? d : d + 1)];
+                p_slope[((long)e * 8 + d) * HW + cell] = oracle_exp_f32(0.078f * s);
+            }
+}
+
+static float clamp01(float v) { return fminf(fmaxf(v, 0.0f), 1.0f); }
+
+/* one env, one step */
+static void alex_env(const oracle_alex_params* p, int e, int H, int W, const uint8_t* g, uint8_t* go,
+                     const int16_t* age, int16_t* ageo, const uint8_t* veg, const uint8_t* den, const uint8_t* dous,
+                     const float* ps, int widx, uint32_t step, const float* ib, const float* ig, const int32_t* ia,
+                     float* po, int32_t* counts) {
+    const long HW = (long)H * W;
+    const int R = p->R;
+    const float in_minus_bd = p->dous_inner - p->dous_border;
+    const uint32_t k0 = (uint32_t)p->seed, k1 = (uint32_t)(p->seed >> 32);
+    const uint32_t env_id = (uint32_t)(p->env_offset + e);
+    float wind[8];
+    for (int d = 0; d < 8; ++d) wind[d] = p->winds[widx][d < 4 ? d : d + 1];
+    int cE = 0, cT = 0, cF = 0;
+    /* summed-area tables of FIRE indicators and dousing values, (H+1) x (W+1) */
+    int64_t* satf = (int64_t*)calloc((size_t)(H + 1) * (W + 1), sizeof(int64_t));
+    int64_t* satd = (int64_t*)calloc((size_t)(H + 1) * (W + 1), sizeof(int64_t));
+    for (int r = 0; r < H; ++r)
+        for (int c = 0; c < W; ++c) {
+            const long i = (long)(r + 1) * (W + 1) + (c + 1);
+            satf[i] = (g[(long)r * W + c] == p->fire) + satf[i - 1] + satf[i - (W + 1)] - satf[i - (W + 1) - 1];
+            satd[i] = dous[(long)r * W + c] + satd[i - 1] + satd[i - (W + 1)] - satd[i - (W + 1) - 1];
+        }
+    for (int r = 0; r < H; ++r) {
+        for (int c = 0; c < W; ++c) {
+            const long cell = (long)r * W + c;
+            /* box sums from the summed-area tables (clamped to the grid = zero padding) */
+            float ph = 0.0f, dz = 0.0f;
+            const int KS = R < 2 ? 2 : R;
+            for (int k = 0; k <= KS; ++k) {
+                const int r0 = r - k < 0 ? 0 : r - k, r1 = r + k + 1 > H ? H : r + k + 1;
+                const int c0 = c - k < 0 ? 0 : c - k, c1 = c + k + 1 > W ? W : c + k + 1;
+                const long W1 = W + 1;
+                const int64_t fire_n = satf[r1 * W1 + c1] - satf[r0 * W1 + c1] - satf[r1 * W1 + c0] + satf[r0 * W1 + c0];
+                const int64_t dsum = satd[r1 * W1 + c1] - satd[r0 * W1 + c1] - satd[r1 * W1 + c0] + satd[r0 * W1 + c0];
+                if (k <= R) ph = ph + p->heat_dw[k] * (float)fire_n;
+                if (k == 1) dz = in_minus_bd * (float)dsum;
+                if (k == 2) dz = dz + p->dous_border * (float)dsum;
+            }
+            ph = ph - dz;
+            /* neighbourhood fire mask, d = (a,b) row-major without the centre */
+            uint32_t fm = 0;
+            int d = 0;
+            for (int a = 0; a < 3; ++a)
+                for (int b = 0; b < 3; ++b) {
+                    if (a == 1 && b == 1) continue;
+                    const int rr = r + a - 1, cc = c + b - 1;
+                    if (rr >= 0 && rr < H && cc >= 0 && cc < W && g[(long)rr * W + cc] == p->fire) fm |= 1u << d;
+                    ++d;
+                }
+            const int vv = veg[cell], dd = den[cell];
+            const int vi = vv < 1 ? 1 : (vv > 5 ? 5 : vv), di = dd < 1 ? 1 : (dd > 5 ? 5 : dd);
+            const float base = (ph * p->veg1p[vi]) * p->den1p[di];
+            float pd[8];
+            for (int q = 0; q < 8; ++q) pd[q] = (base * wind[q]) * ps[(long)q * HW + cell];
+            if (po)
+                for (int q = 0; q < 8; ++q) po[cell * 8 + q] = pd[q];
+            const int x = g[cell];
+            const int is_tree = x == p->tree, is_empty = x == p->empty, is_fire = x == p->fire;
+            int burn = 0, grow = 0, new_age = p->age_lo;
+            if (ib) {
+                if (is_tree && fm) {
+                    for (int q = 0; q < 8; ++q)
+                        if (((fm >> q) & 1u) && ib[cell * 9 + (q < 4 ? q : q + 1)] < pd[q]) burn = 1;
+                    if (burn) new_age = ia[cell];
+                }
+                if (is_empty) grow = ig[cell] < p->p_tree;
+            } else if ((is_tree && fm) || (is_empty && p->p_tree > 0.0f)) {
+                const uint32_t ctr[4] = {(uint32_t)cell, env_id, step, TAG_ALEX_CELL};
+                uint32_t rx[4];
+                philox(ctr, k0, k1, rx);
+                if (is_tree) {
+                    float qn = 1.0f;
+                    for (int q = 0; q < 8; ++q)
+                        if ((fm >> q) & 1u) qn = qn * (1.0f - clamp01(pd[q]));
+                    burn = u01(rx[0]) < 1.0f - qn;
+                    new_age = randint_ms(rx[2], p->age_lo, p->age_hi);
+                } else {
+                    grow = u01(rx[1]) < p->p_tree;
+                }
+            }
+            int nx = x;
+            if (is_tree && burn) nx = p->fire;
+            else if (is_empty && grow) nx = p->tree;
+            else if (is_fire && age[cell] <= 1) nx = p->empty;
+            int na = (nx == p->fire && !is_fire) ? new_age : age[cell];
+            if (is_fire) na -= 1;
+            go[cell] = (uint8_t)nx;
+            ageo[cell] = (int16_t)na;
+            cE += nx == p->empty;
+            cT += nx == p->tree;
+            cF += nx == p->fire;
+        }
+    }
+    free(satf);
+    free(satd);
+    if (counts) {
+        counts[0] = cE;
+        counts[1] = cT;
+        counts[2] = cF;
+    }
+}
+
+void oracle_alex_step(const oracle_alex_params* p, int E, int H, int W, const uint8_t* grid_in, uint8_t* grid_out,
+                      const int16_t* age_in, int16_t* age_out, const uint8_t* veg, const uint8_t* den,
+                      const uint8_t* dousing, const float* p_slope, const int32_t* wind_index,
+                      const uint32_t* rng_step, const float* inj_burn, const float* inj_grow, const int32_t* inj_age,
+                      float* prob_out, int32_t* counts) {
+    const long HW = (long)H * W;
+    for (int e = 0; e < E; ++e) {
+        alex_env(p, e, H, W, grid_in + e * HW, grid_out + e * HW, age_in + e * HW, age_out + e * HW, veg + e * HW,
+                 den + e * HW, dousing + e * HW, p_slope + e * 8 * HW, wind_index[e], rng_step ? rng_step[e] : 0u,
+                 inj_burn ? inj_burn + e * HW * 9 : 0, inj_grow ? inj_grow + e * HW : 0,
+                 inj_age ? inj_age + e * HW : 0, prob_out ? prob_out + e * HW * 8 : 0, counts ? counts + 3 * e : 0);
+    }
+}
+
+/* wind change (ca_alexandridis_jax.py:442-451) with the device's Philox convention */
+void oracle_alex_wind_change(float p_change, int n_winds, uint64_t seed, int env_offset, const uint32_t* rng_step,
+                             int32_t* wind_index, int E) {
+    for (int e = 0; e < E; ++e) {
+        const uint32_t ctr[4] = {0u, (uint32_t)(env_offset + e), rng_step ? rng_step[e] : 0u, TAG_ALEX_WIND};
+        uint32_t x[4];
+        philox(ctr, (uint32_t)seed, (uint32_t)(seed >> 32), x);
+        if (u01(x[0]) < p_change) wind_index[e] = (wind_index[e] + randint_ms(x[1], 1, 8)) % n_winds;
+    }
+}

@@ -1,0 +1,86 @@
+"""The C-ABI library loads and exports every symbol include/gca.h declares; ctypes
+struct layouts equal the C compiler's. No compute calls (no GPU needed)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "gca.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(gca_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    from gymca_amd import _lib
+
+    lib = _lib.load()
+    names = declared_functions()
+    assert len(names) >= 20
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    assert set(names) == set(_lib.EXPORTED_SYMBOLS), set(names) ^ set(_lib.EXPORTED_SYMBOLS)
+
+
+def test_version_and_error_calls_need_no_gpu():
+    from gymca_amd import _lib
+
+    lib = _lib.load()
+    assert lib.gca_version() == 1
+    assert isinstance(lib.gca_last_error(), bytes)
+
+
+def test_argument_errors_are_reported_without_touching_the_gpu():
+    from gymca_amd import _lib
+
+    with pytest.raises(_lib.GCAError, match="E, H, W must be positive"):
+        _lib.call("gca_windy_step", 1, 1, None, None, 0, 1, 0, 4, 4, 0, 3, 25, 0, None, None)
+    with pytest.raises(_lib.GCAError, match="burn radius"):
+        p = _lib.AlexParams()
+        p.R = 0
+        _lib.call("gca_alex_step", p, 1, 4, 4, *([1] * 9), None, None, None, None, None, None, None)
+
+
+C_LAYOUT = r"""
+#include <stdio.h>
+#include <stddef.h>
+#include "gca.h"
+#define P(T, f) printf("%s.%s %zu\n", #T, #f, offsetof(T, f));
+int main(void) {
+  printf("gca_bulldozer_params %zu\n", sizeof(gca_bulldozer_params));
+  P(gca_bulldozer_params, t_shoot) P(gca_bulldozer_params, seed) P(gca_bulldozer_params, right_mask)
+  P(gca_bulldozer_params, effect)
+  printf("gca_alex_params %zu\n", sizeof(gca_alex_params));
+  P(gca_alex_params, heat_dw) P(gca_alex_params, p_tree) P(gca_alex_params, seed) P(gca_alex_params, n_winds)
+  P(gca_alex_params, winds)
+  printf("gca_advenv_params %zu\n", sizeof(gca_advenv_params));
+  P(gca_advenv_params, day_length) P(gca_advenv_params, seed) P(gca_advenv_params, right_mask)
+  return 0;
+}
+"""
+
+
+def test_struct_layouts_match_the_header(tmp_path):
+    from gymca_amd import _lib
+
+    src = tmp_path / "layout.c"
+    src.write_text(C_LAYOUT)
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    got = dict(line.rsplit(" ", 1) for line in out if line)
+    py = {"gca_bulldozer_params": _lib.BulldozerParams, "gca_alex_params": _lib.AlexParams,
+          "gca_advenv_params": _lib.AdvEnvParams}
+    for key, val in got.items():
+        if "." in key:
+            t, f = key.split(".")
+            assert getattr(py[t], f).offset == int(val), key
+        else:
+            assert ctypes.sizeof(py[key]) == int(val), key

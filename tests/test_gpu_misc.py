@@ -1,0 +1,105 @@
+"""GPU: count_cells, Move/Modify drop-ins vs the reference's golden rows, Drossel-Schwabl and
+the helicopter env vs the seeded reference, reset_where."""
+import numpy as np
+import pytest
+
+from _contract import assert_operator
+
+pytestmark = pytest.mark.gpu
+
+
+def test_count_cells_matches_numpy(device):
+    import torch
+
+    from gymca_amd import _device as dev
+    from gymca_amd._lib import call
+
+    for E, H, W in [(3, 17, 29), (5, 256, 256), (2, 1, 1), (4, 64, 48)]:
+        g = np.random.default_rng(E).choice(np.array([0, 3, 25, 7], np.uint8), size=(E, H, W))
+        gd = torch.as_tensor(g, device=device)
+        c = torch.zeros((E, 3), dtype=torch.int32, device=device)
+        call("gca_count_cells", dev.ptr(gd), E, H, W, 0, 3, 25, dev.ptr(c), dev.stream_ptr())
+        exp = np.stack([(g == v).sum(axis=(1, 2)) for v in (0, 3, 25)], axis=1)
+        assert np.array_equal(c.cpu().numpy(), exp)
+
+
+def test_move_modify_dropins_match_reference_rows(golden, device):
+    from gymca_amd.forest_fire.operators import Modify, Move, MoveModify
+
+    sets = {"up": {0, 1, 2}, "down": {6, 7, 8}, "left": {0, 3, 6}, "right": {2, 5, 8}, "not_move": {4}}
+    mm = MoveModify(Move(sets), Modify({3: 0}))
+    rows = golden("move_modify")["rows"]
+    rng = np.random.default_rng(0)
+    for H, W, r, c, a, shoot, pr, pc, before, after, hit in rows[rng.choice(len(rows), 300, replace=False)]:
+        grid = np.zeros((H, W), dtype=np.int64)
+        grid[pr, pc] = before
+        g, pos = mm(grid, (int(a), int(shoot)), np.array([r, c]))
+        assert tuple(pos) == (pr, pc) and g is grid and grid[pr, pc] == after and mm.modify.hit == bool(hit)
+
+
+def test_modify_cyclic_effects_reference_test(device):
+    """test_move_modify.py:92-125: cyclic effects on a 3-state grid, in place."""
+    from gymca_amd.forest_fire.operators import Modify
+    from gymca_amd.grid_space import GridSpace
+
+    effects = {s: range(3)[s - 2] for s in range(3)}
+    modify = Modify(effects)
+    assert_operator(modify, strict=False)
+    gs = GridSpace(n=3, shape=(3, 3))
+    rng = np.random.default_rng(2)
+    for _ in range(16):
+        for action in (True, False):
+            grid = gs.sample()
+            pos = rng.integers(0, 3, 2)
+            target = grid[pos[0], pos[1]]
+            g, p = modify(grid, action, pos)
+            assert g[pos[0], pos[1]] == (effects[target] if action else target) and np.all(p == pos)
+
+
+def test_drossel_dropin_matches_seeded_reference(golden, device):
+    from gymca_amd.forest_fire.operators import ForestFire
+
+    d = golden("drossel")
+    for i in range(int(d["n"])):
+        op = ForestFire(0, 1, 2)
+        op.seed(int(d[f"c{i}_seed"]))
+        out, _ = op.update(d[f"c{i}_grid"].astype(np.int64), None, d[f"c{i}_p"])
+        assert np.array_equal(out, d[f"c{i}_out"]), f"case {i}"
+
+
+def test_helicopter_env_replays_seeded_reference(golden, device):
+    from gymca_amd.forest_fire.helicopter import ForestFireHelicopterEnv
+
+    d = golden("helicopter")
+    env = ForestFireHelicopterEnv(5, 5)
+    env.reset(seed=7)
+    env.cellular_automaton.seed(int(d["seed"]))
+    env.grid = d["grid0"].astype(np.int64)
+    ca_params, pos, freeze = env.context
+    env.context = (ca_params, pos, freeze)
+    for s in range(len(d["grids"])):
+        obs, rew, term, trunc, info = env.step(s % 9)
+        grid, (cp, pos, fr) = obs
+        assert np.array_equal(grid, d["grids"][s]), f"step {s}"
+        exp = d["recs"][s]
+        assert np.isclose(rew, exp[0], rtol=0, atol=1e-15) and (pos[0], pos[1], int(fr)) == (exp[1], exp[2], exp[3])
+        assert bool(info["hit"]) == bool(exp[4])
+
+
+def test_reset_where(device):
+    import torch
+
+    from gymca_amd import _device as dev
+    from gymca_amd._lib import call
+
+    E, H, W = 5, 19, 23
+    g = torch.randint(0, 3, (E, H, W), dtype=torch.uint8, device=device)
+    g0 = torch.randint(0, 3, (E, H, W), dtype=torch.uint8, device=device)
+    done = torch.tensor([0, 1, 0, 1, 1], dtype=torch.uint8, device=device)
+    ref = torch.where(done.bool()[:, None, None], g0, g)
+    pos = torch.zeros((E, 2), dtype=torch.int32, device=device)
+    pos0 = torch.ones((E, 2), dtype=torch.int32, device=device)
+    call("gca_reset_where", dev.ptr(done), E, H, W, dev.ptr(g), dev.ptr(g0), None, None, None, None, dev.ptr(pos),
+         dev.ptr(pos0), None, None, None, dev.stream_ptr())
+    assert torch.equal(g, ref) and int(done.sum()) == 0
+    assert pos[:, 0].tolist() == [0, 1, 0, 1, 1]

@@ -1,0 +1,224 @@
+"""GPU parity: WindyForestFire kernels and the ForestFireBulldozer envs vs the reference
+(golden vectors) and the CPU oracle (Philox rolls). Bit-exact integer states."""
+import numpy as np
+import pytest
+
+from _contract import assert_operator
+from oracle import windy as owindy
+
+pytestmark = pytest.mark.gpu
+
+
+def _torch():
+    import torch
+
+    return torch
+
+
+def test_windy_dropin_matches_reference_golden(golden, device):
+    from gymca_amd.forest_fire.operators import WindyForestFire
+
+    d = golden("windy")
+    for i in range(int(d["n"])):
+        E, T, F = (int(v) for v in d[f"c{i}_values"])
+        op = WindyForestFire(E, T, F)
+        grid = d[f"c{i}_grid"].astype(np.int64)
+        out, w = op.update(grid, None, d[f"c{i}_wind"], roll=d[f"c{i}_roll"])
+        assert out.dtype == np.int64
+        assert np.array_equal(out, d[f"c{i}_out"]), f"case {i} shape {grid.shape} values {(E, T, F)}"
+
+
+def test_windy_dict_context_is_unwrapped(device):
+    from gymca_amd.forest_fire.operators import WindyForestFire
+
+    op = WindyForestFire()
+    g = np.full((8, 8), 3)
+    g[4, 4] = 25
+    ctx = {"wind": np.ones((3, 3))}
+    out, ctx_out = op.update(g, None, ctx)
+    assert ctx_out is ctx
+    assert out[4, 4] == 0 and np.all(out[3:6, 3:6][np.array([[1, 1, 1], [1, 0, 1], [1, 1, 1]], bool)] == 25)
+
+
+@pytest.mark.parametrize("W", [16, 32, 64, 128, 256, 512, 1024])
+def test_fast_kernel_equals_exact_kernel(device, W):
+    torch = _torch()
+    from gymca_amd import _device as dev
+    from gymca_amd._lib import call
+
+    E, H = 7, 45 if W < 1024 else 19
+    rng = np.random.default_rng(W)
+    grid = rng.choice(np.array([0, 3, 25], np.uint8), size=(E, H, W), p=[0.2, 0.5, 0.3])
+    masks = torch.as_tensor(rng.integers(0, 256, E).astype(np.uint8), device=device)
+    src = torch.as_tensor(grid, device=device)
+    outs, cnts = [], []
+    for exact in (0, 1):
+        dst = torch.zeros_like(src)
+        counts = torch.zeros((E, 3), dtype=torch.int32, device=device)
+        call("gca_windy_step", dev.ptr(src), dev.ptr(dst), None, None, 0, dev.ptr(masks), E, H, W, 0, 3, 25, exact,
+             dev.ptr(counts), dev.stream_ptr())
+        outs.append(dst.cpu().numpy())
+        cnts.append(counts.cpu().numpy())
+    assert np.array_equal(outs[0], outs[1])
+    assert np.array_equal(cnts[0], cnts[1])
+    # and the oracle (scipy convolve2d restatement) agrees
+    for e in (0, E - 1):
+        m = int(masks[e].item())
+        roll = np.full((3, 3), 0.5)
+        wind = np.zeros((3, 3))
+        for d, idx in enumerate([0, 1, 2, 3, 5, 6, 7, 8]):
+            wind.reshape(9)[idx] = 1.0 if (m >> d) & 1 else 0.0
+        ref = owindy.windy_step(grid[e].astype(np.int64), wind, roll)
+        assert np.array_equal(outs[0][e], ref)
+        assert tuple(cnts[0][e]) == tuple(int(np.sum(ref == v)) for v in (0, 3, 25))
+
+
+def test_philox_dirmask_matches_oracle(device):
+    torch = _torch()
+    from gymca_amd import _device as dev
+    from gymca_amd._lib import call
+
+    E, seed = 50, 0x5EED
+    rng = np.random.default_rng(3)
+    wind = rng.random((E, 9))
+    w_d = torch.as_tensor(wind, device=device)
+    for step in (0, 1, 77):
+        rs = torch.full((E,), step, dtype=torch.int32, device=device)
+        m = torch.zeros(E, dtype=torch.uint8, device=device)
+        call("gca_windy_dirmask", dev.ptr(w_d), 9, None, seed, dev.ptr(rs), None, 0, 100, dev.ptr(m), E,
+             dev.stream_ptr())
+        got = m.cpu().numpy()
+        for e in range(E):
+            assert got[e] == owindy.dir_mask(wind[e], owindy.philox_roll(seed, 100 + e, step))
+
+
+@pytest.mark.parametrize("N,E,steps", [(32, 6, 120), (64, 4, 80), (256, 3, 60), (40, 5, 60)])
+def test_batched_bulldozer_env_matches_oracle(device, N, E, steps):
+    from gymca_amd.forest_fire.bulldozer import BatchedForestFireBulldozerEnv
+
+    env = BatchedForestFireBulldozerEnv(E, N, N, device=device, seed=17)
+    env.reset(seed=5)
+    grids0 = env.grids().cpu().numpy()
+    pos0 = env.pos.cpu().numpy()
+    o = owindy.BulldozerOracle(grids0, pos0, env.wind[0].cpu().numpy().reshape(3, 3), env.t_act_move,
+                               env.t_act_shoot, env.t_any, seed=17)
+    rng = np.random.default_rng(1)
+    for s in range(steps):
+        act = np.stack([rng.integers(0, 9, E), rng.integers(0, 2, E)], axis=1)
+        _, rew, term, _, info = env.step(act)
+        exp = o.step(act)
+        got = env.grids().cpu().numpy()
+        for e in range(E):
+            assert np.array_equal(got[e], o.grids[e]), f"step {s} env {e}"
+        r = rew.cpu().numpy()
+        assert np.array_equal(np.isnan(r), np.isnan(exp)) and np.allclose(r[~np.isnan(r)], exp[~np.isnan(exp)],
+                                                                           rtol=0, atol=0)
+        assert np.array_equal(term.cpu().numpy(), o.done)
+        assert np.array_equal(env.pos.cpu().numpy(), np.array(o.pos))
+        assert np.array_equal(env.accu.cpu().numpy(), o.accu)
+        assert np.array_equal(env.hit.cpu().numpy().astype(bool), o.hit)
+
+
+@pytest.mark.parametrize("case", [0, 1, 2])
+def test_dropin_bulldozer_env_replays_reference_episode(golden, device, case):
+    import zlib
+
+    from gymca_amd.forest_fire.bulldozer import ForestFireBulldozerEnv
+
+    d = golden("bulldozer")
+    N = int(d[f"c{case}_N"])
+    env = ForestFireBulldozerEnv(N, N)
+    env.reset(seed=0)
+    env.grid = d[f"c{case}_grid0"].astype(np.int64)
+    env.context = ({"wind": d[f"c{case}_wind"]}, d[f"c{case}_pos0"].astype(np.int64), np.array(0.0))
+    env.state = env.grid, env.context
+    rolls, nrolls = d[f"c{case}_rolls"], d[f"c{case}_nrolls"]
+    k = 0
+    for s, (act, rec) in enumerate(zip(d[f"c{case}_actions"], d[f"c{case}_recs"])):
+        env.ca.roll_queue = list(rolls[k:k + nrolls[s]])
+        k += nrolls[s]
+        obs, rew, term, trunc, info = env.step(act)
+        grid, (ca_params, pos, t) = obs
+        exp_rew, exp_term, exp_hit, pr, pc, tt, cE, cT, cF = rec
+        assert rew == exp_rew and bool(term) == bool(exp_term) and bool(info["hit"]) == bool(exp_hit), f"step {s}"
+        assert (int(pos[0]), int(pos[1])) == (pr, pc) and float(t) == tt
+        assert zlib.crc32(np.asarray(grid).astype(np.uint8).tobytes()) & 0xFFFFFFFF == int(d[f"c{case}_crc"][s])
+        assert not env.ca.roll_queue
+
+
+def test_operator_contracts(device):
+    from gymca_amd.forest_fire.bulldozer import ForestFireBulldozerEnv
+    from gymca_amd.forest_fire.operators import WindyForestFire
+
+    assert_operator(WindyForestFire(0, 3, 25), strict=False)
+    env = ForestFireBulldozerEnv(nrows=32, ncols=32)
+    assert_operator(env.MDP, strict=True)
+
+
+def test_reference_windy_invariants_deterministic_wind(device):
+    """test_ca_windy.py:55-102 restated: wind = 1 everywhere -> exact rule checks."""
+    from gymca_amd.forest_fire.operators import WindyForestFire
+    from gymca_amd.grid_space import GridSpace
+
+    ca = WindyForestFire(0, 3, 25)
+    wind = ca.context_space.high
+    gs = GridSpace(values=[0, 3, 25], shape=(4, 4))
+    for _ in range(16):
+        grid = gs.sample()
+        for _ in range(4):
+            new, _ = ca(grid, None, wind)
+            pad = np.pad(grid, 1)
+            for r in range(4):
+                for c in range(4):
+                    nb = pad[r:r + 3, c:c + 3]
+                    if grid[r, c] == 3:
+                        assert new[r, c] == (25 if (nb == 25).any() else 3)
+                    else:
+                        assert new[r, c] == 0
+            grid = new
+
+
+def test_reference_repeat_ca_two_steps(device):
+    """test_repeat_ca.py:68-90: time 1.0 + 1.0 -> exactly two CA applications, accu back to 0."""
+    from gymca_amd.forest_fire.operators import RepeatCA, WindyForestFire
+    from gymca_amd.grid_space import GridSpace
+    from gymca_amd.spaces import Box, Discrete, Tuple
+
+    gs = GridSpace(values=[0, 3, 25], shape=(8, 8))
+    ca = WindyForestFire(0, 3, 25, grid_space=gs, action_space=Discrete(1))
+    ctx = Tuple((ca.context_space, Box(np.array(0.0), np.array(1.0), dtype=np.float64)))
+    rep = RepeatCA(ca, lambda a: 1.0, lambda s: 1.0, grid_space=gs, action_space=Discrete(1), context_space=ctx)
+    assert_operator(rep, strict=True)
+    grid = gs.sample()
+    params = ca.context_space.high
+    observed, (_, accu) = rep(grid.copy(), None, (params, 0.0))
+    g2, _ = ca(grid.copy(), None, params)
+    g2, _ = ca(g2, None, params)
+    assert np.array_equal(observed, g2) and accu == 0.0
+
+
+def test_full_size_windy_properties(device):
+    """BASELINE config 2 size (1024 x 256^2) through the batched env's forced CA step:
+    FIRE -> EMPTY, EMPTY stays, counts add up, and a sampled env equals the oracle."""
+    torch = _torch()
+    from gymca_amd.forest_fire.bulldozer import BatchedForestFireBulldozerEnv
+
+    E, N = 1024, 256
+    env = BatchedForestFireBulldozerEnv(E, N, N, device=device, seed=3, p_tree=0.6, p_empty=0.1)
+    env.reset()
+    # dense variant: sprinkle fire
+    g = env.grids()
+    g[torch.rand(g.shape, device=device) < 0.3] = 25
+    env.buf[0].copy_(g)
+    env.dir_mask.copy_(torch.randint(0, 256, (E,), dtype=torch.uint8, device=device))
+    before = env.grids().clone()
+    env.ca_step_all()
+    after = env.grids()
+    assert torch.all(after[before == 25] == 0) and torch.all(after[before == 0] == 0)
+    assert torch.all((after[before == 3] == 3) | (after[before == 3] == 25))
+    for e in (0, 511, 1023):
+        m = int(env.dir_mask[e].item())
+        wind = np.array([1.0 if (m >> d) & 1 else 0.0 for d in range(8)])
+        w9 = np.insert(wind, 4, 0.0).reshape(3, 3)
+        ref = owindy.windy_step(before[e].cpu().numpy().astype(np.int64), w9, np.full((3, 3), 0.5))
+        assert np.array_equal(after[e].cpu().numpy(), ref)
