@@ -27,26 +27,44 @@ namespace {
 constexpr int TH = 16;
 constexpr int TW = 256;
 constexpr int CW = TW + 32;  // staged columns: [c0-16, c0+TW+16)
+// LDS row layout of the column prefix: one pad dword after every 16 columns (column c at
+// c + c/16) and a row stride = 16 (mod 32) dwords, so the 64 lanes of a heat-window read
+// (4 rows x 16 lanes, 16 columns apart) hit 64 distinct banks of a ds_read_b32 lane group.
+constexpr int CWP = 336;
+__host__ __device__ constexpr int pcol(int c) { return c + (c >> 4); }
+static_assert(pcol(CW - 1) < CWP && CWP % 32 == 16, "padded row");
 
 __device__ __forceinline__ float clamp01(float v) { return fminf(fmaxf(v, 0.0f), 1.0f); }
 
-template <int R, bool INJECT>
-__global__ __launch_bounds__(256, 2) void alex_step_kernel(
+// MODE: 0 = Philox draws (production), 1 = Philox + debug burn probabilities, 2 = injected draws
+// (+ probabilities when prob_out != NULL). The debug store is compiled out of mode 0.
+template <int R, int MODE>
+__global__ __launch_bounds__(256, 4) void alex_step_kernel(
     gca_alex_params p, int H, int W, int tiles_r, int tiles_c, const uint8_t* __restrict__ grid_in,
     uint8_t* __restrict__ grid_out, const int16_t* __restrict__ age_in, int16_t* __restrict__ age_out,
     const uint8_t* __restrict__ veg, const uint8_t* __restrict__ den, const uint8_t* __restrict__ dousing,
     const float* __restrict__ p_slope, const int32_t* __restrict__ wind_index, const uint32_t* __restrict__ rng_step,
     const float* __restrict__ inj_burn, const float* __restrict__ inj_grow, const int32_t* __restrict__ inj_age,
     float* __restrict__ prob_out, int32_t* __restrict__ counts) {
+    constexpr bool INJECT = MODE == 2;
+    constexpr bool PROB = MODE != 0;
     constexpr int RS = R < 2 ? 2 : R;  // staged halo: heat radius, at least the 5x5 dousing box
     constexpr int RR = TH + 2 * RS;    // staged rows
+    constexpr int NCH = CW / 16;       // 16-column chunks per staged row
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    uint32_t* CP = reinterpret_cast<uint32_t*>(smem);            // [RR+1][CW]
-    uint8_t* G = smem + sizeof(uint32_t) * (RR + 1) * CW;        // [RR][CW]
+    uint32_t* CP = reinterpret_cast<uint32_t*>(smem);                             // [RR+1][CWP] column prefix
+    uint16_t* FB = reinterpret_cast<uint16_t*>(smem + sizeof(uint32_t) * (RR + 1) * CWP);  // [RR][NCH] fire bits
 
+    // XCD-aware order: blocks b, b+8, b+16, ... share an XCD (and its L2) under round-robin
+    // dispatch; give each XCD a contiguous range of (env, tile) so the halo rows a tile stages
+    // were just fetched into the same L2 by its neighbour tile. Bijective for any grid size.
     const int tiles = tiles_r * tiles_c;
-    const int e = blockIdx.x / tiles;
-    const int tile = blockIdx.x - e * tiles;
+    const int nb = (int)gridDim.x;
+    const int xcd = (int)blockIdx.x & 7, slot = (int)blockIdx.x >> 3;
+    const int qn8 = nb >> 3, rn8 = nb & 7;
+    const int lb = (xcd < rn8 ? xcd * (qn8 + 1) : rn8 * (qn8 + 1) + (xcd - rn8) * qn8) + slot;
+    const int e = lb / tiles;
+    const int tile = lb - e * tiles;
     const int r0 = (tile / tiles_c) * TH, c0 = (tile % tiles_c) * TW;
     const int64_t HW = (int64_t)H * W;
     const uint8_t* gE = grid_in + (int64_t)e * HW;
@@ -56,52 +74,57 @@ __global__ __launch_bounds__(256, 2) void alex_step_kernel(
                         ((((uintptr_t)grid_in) | ((uintptr_t)dousing) | ((uintptr_t)grid_out) | ((uintptr_t)veg) |
                           ((uintptr_t)den) | ((uintptr_t)age_in) | ((uintptr_t)age_out) | ((uintptr_t)p_slope)) &
                          15u) == 0;
+    const uint32_t Fp = rep4((uint32_t)p.fire), Ep = rep4((uint32_t)p.empty);
 
-    // ---------------- per-thread cells
+    // ---------------- this thread's 16 cells: row r, columns [cbase, cbase+16)
     const int tr = tid >> 4, q = tid & 15;
     const int r = r0 + tr;
     const int cbase = c0 + 16 * q;
     const bool row_ok = r < H;
-    const int rr = RS + tr;          // staged row of r
-    const int cc0 = 16 + 16 * q;     // staged column of cbase
-
-    // ---- per-cell contexts (packed)
-    const int64_t rowoff = (int64_t)e * HW + (int64_t)r * W + cbase;
+    const int rr = RS + tr;  // staged row of r
+    // global addressing: wave-uniform per-env base pointers (SGPRs) + 32-bit lane offsets,
+    // so no 64-bit address VGPRs stay live across the kernel
+    const uint32_t lo = (uint32_t)(r * W + cbase);  // cell offset of cell 0 within the env
+    const uint8_t* gEi = grid_in + (size_t)e * HW;
+    const int16_t* aEi = age_in + (size_t)e * HW;
+    const uint8_t* vE = veg + (size_t)e * HW;
+    const uint8_t* nE = den + (size_t)e * HW;
+    const int64_t rowoff = (int64_t)e * HW + lo;  // debug / injected arrays only
     const bool vec = row_ok && rows16 && (cbase + 16 <= W);
-    uint32_t agew[8], vgw[4], dnw[4];
+
+    // per-cell inputs, issued before the LDS phases so their latency overlaps them
+    // (fire ages are loaded later, after the direction pass, to keep them out of its VGPR peak)
+    uint32_t own[4], vgw[4], dnw[4];
     if (vec) {
-        const uint4 a0 = *reinterpret_cast<const uint4*>(age_in + rowoff);
-        const uint4 a1 = *reinterpret_cast<const uint4*>(age_in + rowoff + 8);
-        const uint4 v4 = *reinterpret_cast<const uint4*>(veg + rowoff);
-        const uint4 d4 = *reinterpret_cast<const uint4*>(den + rowoff);
-        agew[0] = a0.x; agew[1] = a0.y; agew[2] = a0.z; agew[3] = a0.w;
-        agew[4] = a1.x; agew[5] = a1.y; agew[6] = a1.z; agew[7] = a1.w;
+        const uint4 g4 = *reinterpret_cast<const uint4*>(gEi + lo);
+        const uint4 v4 = *reinterpret_cast<const uint4*>(vE + lo);
+        const uint4 d4 = *reinterpret_cast<const uint4*>(nE + lo);
+        own[0] = g4.x; own[1] = g4.y; own[2] = g4.z; own[3] = g4.w;
         vgw[0] = v4.x; vgw[1] = v4.y; vgw[2] = v4.z; vgw[3] = v4.w;
         dnw[0] = d4.x; dnw[1] = d4.y; dnw[2] = d4.z; dnw[3] = d4.w;
     } else {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) agew[k] = 0u;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) vgw[k] = dnw[k] = 0x01010101u;
+        for (int k = 0; k < 4; ++k) {
+            vgw[k] = dnw[k] = 0x01010101u;
+            own[k] = Ep;
+        }
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
             if (row_ok && cbase + i < W) {
-                agew[i >> 1] |= (uint32_t)(uint16_t)age_in[rowoff + i] << (16 * (i & 1));
                 const uint32_t sh = 8 * (i & 3);
-                vgw[i >> 2] = (vgw[i >> 2] & ~(0xFFu << sh)) | ((uint32_t)veg[rowoff + i] << sh);
-                dnw[i >> 2] = (dnw[i >> 2] & ~(0xFFu << sh)) | ((uint32_t)den[rowoff + i] << sh);
+                vgw[i >> 2] = (vgw[i >> 2] & ~(0xFFu << sh)) | ((uint32_t)vE[lo + i] << sh);
+                dnw[i >> 2] = (dnw[i >> 2] & ~(0xFFu << sh)) | ((uint32_t)nE[lo + i] << sh);
+                own[i >> 2] = (own[i >> 2] & ~(0xFFu << sh)) | ((uint32_t)gEi[lo + i] << sh);
             }
         }
     }
 
-    // ---------------- stage: grid bytes -> G, packed fire|dousing<<16 -> CP rows 1..RR
-    const uint32_t Fp = rep4((uint32_t)p.fire);
-    for (int ch = tid; ch < RR * (CW / 16); ch += 256) {
-        const int rr = ch / (CW / 16), cq = ch - rr * (CW / 16);
-        const int gr = r0 - RS + rr, gc = c0 - 16 + 16 * cq;
-        uint32_t gw[4] = {0u, 0u, 0u, 0u}, dw[4] = {0u, 0u, 0u, 0u};
-        const uint32_t Ep = rep4((uint32_t)p.empty);
-        gw[0] = gw[1] = gw[2] = gw[3] = Ep;
+    // ---------------- stage rows [r0-RS, r0+TH+RS) x cols [c0-16, c0+TW+16):
+    //                  packed fire | dousing<<16 -> CP rows 1..RR, fire bitmask -> FB
+    for (int ch = tid; ch < RR * NCH; ch += 256) {
+        const int sr = ch / NCH, cq = ch - sr * NCH;
+        const int gr = r0 - RS + sr, gc = c0 - 16 + 16 * cq;
+        uint32_t gw[4] = {Ep, Ep, Ep, Ep}, dw[4] = {0u, 0u, 0u, 0u};
         if (gr >= 0 && gr < H) {
             if (rows16 && gc >= 0 && gc + 16 <= W) {
                 const uint4 a = *reinterpret_cast<const uint4*>(gE + (int64_t)gr * W + gc);
@@ -120,56 +143,41 @@ __global__ __launch_bounds__(256, 2) void alex_step_kernel(
                 }
             }
         }
-        *reinterpret_cast<uint4*>(G + rr * CW + 16 * cq) = make_uint4(gw[0], gw[1], gw[2], gw[3]);
-        uint32_t* cp = CP + (rr + 1) * CW + 16 * cq;
+        uint32_t* cp = CP + (sr + 1) * CWP + 17 * cq;  // = pcol(16 * cq)
+        uint32_t bits = 0u;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const uint32_t f = bytes_eq01(gw[j], Fp);
-            uint4 v;
-            v.x = (f & 1u) | ((dw[j] & 0xFFu) << 16);
-            v.y = ((f >> 8) & 1u) | (((dw[j] >> 8) & 0xFFu) << 16);
-            v.z = ((f >> 16) & 1u) | (((dw[j] >> 16) & 0xFFu) << 16);
-            v.w = ((f >> 24) & 1u) | (((dw[j] >> 24) & 0xFFu) << 16);
-            *reinterpret_cast<uint4*>(cp + 4 * j) = v;
+            bits |= ((f & 1u) | ((f >> 7) & 2u) | ((f >> 14) & 4u) | ((f >> 21) & 8u)) << (4 * j);
+            cp[4 * j + 0] = (f & 1u) | ((dw[j] & 0xFFu) << 16);
+            cp[4 * j + 1] = ((f >> 8) & 1u) | (((dw[j] >> 8) & 0xFFu) << 16);
+            cp[4 * j + 2] = ((f >> 16) & 1u) | (((dw[j] >> 16) & 0xFFu) << 16);
+            cp[4 * j + 3] = ((f >> 24) & 1u) | (((dw[j] >> 24) & 0xFFu) << 16);
         }
+        FB[sr * NCH + cq] = (uint16_t)bits;
     }
-    for (int cc = tid; cc < CW; cc += 256) CP[cc] = 0u;
+    for (int cc = tid; cc < CWP; cc += 256) CP[cc] = 0u;
     __syncthreads();
-    // ---------------- column prefix (in place)
-    for (int cc = tid; cc < CW; cc += 256) {
-        uint32_t run = 0u;
-#pragma unroll 4
-        for (int rr = 1; rr <= RR; ++rr) {
-            run += CP[rr * CW + cc];
-            CP[rr * CW + cc] = run;
+    // ---------------- column prefix: columns t and t + CW/2 per thread, every load before the adds
+    if (tid < CW / 2) {
+        const int pa = pcol(tid), pb = pcol(tid + CW / 2);
+        uint32_t va[RR], vb[RR];
+#pragma unroll
+        for (int k = 0; k < RR; ++k) {
+            va[k] = CP[(k + 1) * CWP + pa];
+            vb[k] = CP[(k + 1) * CWP + pb];
+        }
+        uint32_t ra = 0u, rb = 0u;
+#pragma unroll
+        for (int k = 0; k < RR; ++k) {
+            ra += va[k];
+            rb += vb[k];
+            CP[(k + 1) * CWP + pa] = ra;
+            CP[(k + 1) * CWP + pb] = rb;
         }
     }
     __syncthreads();
 
-    // ---- 3x3 neighbour FIRE mask per cell, one byte per cell: bit d = neighbourhood entry
-    //      (a,b) row-major without the centre, entry (a,b) = cell (r+a-1, c+b-1) (:332-337)
-    uint32_t fm[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        const uint8_t* gp = G + (rr - 1 + a) * CW + cc0 - 4;
-        const uint4 mid = *reinterpret_cast<const uint4*>(gp + 4);
-        const uint32_t f[6] = {bytes_eq01(*reinterpret_cast<const uint32_t*>(gp), Fp), bytes_eq01(mid.x, Fp),
-                               bytes_eq01(mid.y, Fp), bytes_eq01(mid.z, Fp), bytes_eq01(mid.w, Fp),
-                               bytes_eq01(*reinterpret_cast<const uint32_t*>(gp + 20), Fp)};
-        const int dbase = a * 3 - (a > 1 ? 1 : 0);  // d of (a, 0)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t left = __builtin_amdgcn_alignbyte(f[j + 1], f[j], 3);   // column c-1
-            const uint32_t right = __builtin_amdgcn_alignbyte(f[j + 2], f[j + 1], 1);  // column c+1
-            fm[j] |= left << dbase;
-            if (a != 1) fm[j] |= f[j + 1] << (dbase + 1);
-            fm[j] |= right << (dbase + (a == 1 ? 1 : 2));
-        }
-    }
-    const uint4 own = *reinterpret_cast<const uint4*>(G + rr * CW + cc0);
-    const uint32_t ownw[4] = {own.x, own.y, own.z, own.w};
-
-    __builtin_amdgcn_sched_barrier(0);
     // ---- heat and dousing from box sums B_k (fire field) and D_1, D_2 (dousing field):
     //   heat = sum_k n_k*w_k = sum_{k=0..R} B_k * dw_k   (dw_k = w_k - w_{k+1}, w_{R+1} = 0: p.heat_dw)
     //   dous = inner*D_1 + border*(D_2 - D_1) = (inner - border)*D_1 + border*D_2
@@ -184,11 +192,17 @@ __global__ __launch_bounds__(256, 2) void alex_step_kernel(
 #pragma unroll
     for (int k = 0; k <= RS; ++k) {
         uint32_t V[16 + 2 * RS];
-        const uint32_t* top = CP + (rr - k) * CW + cc0 - k;
-        const uint32_t* bot = CP + (rr + k + 1) * CW + cc0 - k;
+        const uint32_t* top = CP + (rr - k) * CWP + 17 * (q + 1);  // = pcol(cc0)
+        const uint32_t* bot = CP + (rr + k + 1) * CWP + 17 * (q + 1);
 #pragma unroll
-        for (int j = 0; j < 16 + 2 * RS; ++j)
-            if (j < 16 + 2 * k) V[j] = bot[j] - top[j];
+        for (int j = 0; j < 16 + 2 * RS; ++j) {
+            if (j < 16 + 2 * k) {
+                const int t = j - k;                        // column cc0 + t, t in [-k, 16 + k)
+                const int off = t + (t >= 16 ? 1 : 0) - (t < 0 ? 1 : 0);  // pcol(cc0 + t) - pcol(cc0)
+                V[j] = bot[off] - top[off];
+            }
+            if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);  // <= 16 LDS reads in flight (VGPR budget)
+        }
         uint32_t s = 0u;
 #pragma unroll
         for (int j = 0; j <= 2 * RS; ++j)
@@ -210,6 +224,15 @@ __global__ __launch_bounds__(256, 2) void alex_step_kernel(
 #pragma unroll
     for (int i = 0; i < 16; ++i) ph[i] = __fsub_rn(ph[i], dz[i]);  // p_h = heat - dousing (:198)
 
+    // ---- FIRE bits of rows r-1, r, r+1: bit j of nbw[a] <-> staged column cc0 - 1 + j (j = 0..17)
+    uint32_t nbw[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const uint16_t* fb = FB + (rr - 1 + a) * NCH + q;
+        nbw[a] = ((uint32_t)fb[0] >> 15) | ((uint32_t)fb[1] << 1) | (((uint32_t)fb[2] & 1u) << 17);
+    }
+    asm volatile("" : "+v"(nbw[0]), "+v"(nbw[1]), "+v"(nbw[2]));  // build the 3 words now (no 9 live halfwords)
+
     const int widx = wind_index[e];
     float wind[8];
 #pragma unroll
@@ -217,99 +240,168 @@ __global__ __launch_bounds__(256, 2) void alex_step_kernel(
     const uint32_t step = rng_step ? rng_step[e] : 0u;
     const uint32_t k0 = (uint32_t)p.seed, k1 = (uint32_t)(p.seed >> 32);
     const uint32_t env_id = (uint32_t)(p.env_offset + e);
-    const bool want_prob = prob_out != nullptr;
+    const bool want_prob = PROB && prob_out != nullptr;
+    const uint32_t lin0 = lo;  // cell index of cell 0 within the env
 
+    // ---- base[i] = (p_h * (1 + p_veg)) * (1 + p_den)   (left-to-right product of :206)
+    uint32_t treebits = 0u, emptybits = 0u, okbits = 0u;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int x = (int)((own[i >> 2] >> (8 * (i & 3))) & 0xFFu);
+        treebits |= (uint32_t)(x == p.tree) << i;
+        emptybits |= (uint32_t)(x == p.empty) << i;
+        okbits |= (uint32_t)(row_ok && cbase + i < W) << i;
+        // lookups with clip(idx, 1, 5) (:176-178) as select chains (no per-lane indexing)
+        const int vv = (int)((vgw[i >> 2] >> (8 * (i & 3))) & 0xFFu), dd = (int)((dnw[i >> 2] >> (8 * (i & 3))) & 0xFFu);
+        const float av = vv <= 1 ? p.veg1p[1] : vv == 2 ? p.veg1p[2] : vv == 3 ? p.veg1p[3] : vv == 4 ? p.veg1p[4] : p.veg1p[5];
+        const float ad = dd <= 1 ? p.den1p[1] : dd == 2 ? p.den1p[2] : dd == 3 ? p.den1p[3] : dd == 4 ? p.den1p[4] : p.den1p[5];
+        ph[i] = __fmul_rn(__fmul_rn(ph[i], av), ad);  // ph now holds base
+    }
+    // burning-neighbour mask of direction d for all 16 cells: bit i <-> cell i
+    // d = (a, b) row-major without the centre; entry (a, b) = cell (r + a - 1, c + b - 1) (:332-337)
+    auto dir_bits = [&](int d) -> uint32_t {
+        const int a = d < 3 ? 0 : (d < 5 ? 1 : 2);
+        const int b = d < 3 ? d : (d == 3 ? 0 : (d == 4 ? 2 : d - 5));
+        return (nbw[a] >> b) & 0xFFFFu;
+    };
+    uint32_t anyfire = 0u;
+#pragma unroll
+    for (int d = 0; d < 8; ++d) anyfire |= dir_bits(d);
+
+    // ---- direction-outer pass: each p_slope row segment (16 floats = 64 B per lane, 1 KiB per
+    //      16 lanes) is read in one burst, so every HBM line is consumed by one wave instruction group
+    float qn[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) qn[i] = 1.0f;
+    uint32_t burnbits = 0u;
+    const float* psE = p_slope + (size_t)e * 8 * HW;  // wave-uniform
+    auto load_ps = [&](int d, float4 (&v)[4]) {
+        const float* src = psE + (uint32_t)(d * (uint32_t)HW) + lo;
+        if (vec) {
+#pragma unroll
+            for (int m = 0; m < 4; ++m) v[m] = *reinterpret_cast<const float4*>(src + 4 * m);
+        } else {
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                float t4[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) t4[j] = (row_ok && cbase + 4 * m + j < W) ? src[4 * m + j] : 0.0f;
+                v[m] = make_float4(t4[0], t4[1], t4[2], t4[3]);
+            }
+        }
+    };
+#pragma unroll
+    for (int d = 0; d < 8; ++d) {
+        float4 psc[4];
+        load_ps(d, psc);
+        const uint32_t fb = dir_bits(d) & treebits & okbits;
+        const float wd = wind[d];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const float4 v4 = psc[i >> 2];
+            const float ps = (i & 3) == 0 ? v4.x : (i & 3) == 1 ? v4.y : (i & 3) == 2 ? v4.z : v4.w;
+            const float pd = __fmul_rn(__fmul_rn(ph[i], wd), ps);
+            if (PROB && want_prob && ((okbits >> i) & 1u)) prob_out[(rowoff + i) * 8 + d] = pd;
+            const bool f = (fb >> i) & 1u;
+            if (INJECT) {
+                if (f && inj_burn[(rowoff + i) * 9 + (d < 4 ? d : d + 1)] < pd) burnbits |= 1u << i;
+            } else {
+                qn[i] = f ? __fmul_rn(qn[i], __fsub_rn(1.0f, clamp01(pd))) : qn[i];
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);  // one direction's 64 B per lane in flight at a time
+    }
+
+    uint32_t agew[8];
+    if (vec) {
+        const uint4 a0 = *reinterpret_cast<const uint4*>(aEi + lo);
+        const uint4 a1 = *reinterpret_cast<const uint4*>(aEi + lo + 8);
+        agew[0] = a0.x; agew[1] = a0.y; agew[2] = a0.z; agew[3] = a0.w;
+        agew[4] = a1.x; agew[5] = a1.y; agew[6] = a1.z; agew[7] = a1.w;
+    } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) agew[k] = 0u;
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            if (row_ok && cbase + i < W) agew[i >> 1] |= (uint32_t)(uint16_t)aEi[lo + i] << (16 * (i & 1));
+    }
+
+    // ---- draws and the rule, two cells (one Philox block) at a time
     uint32_t outw[4] = {0u, 0u, 0u, 0u}, nagew[8];
     int cntT = 0, cntF = 0, cntE = 0;
-    const float* ps_base = p_slope + ((int64_t)e * 8 * H + r) * W + cbase;  // + d*HW
-
 #pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-        float ps[8][4];
+    for (int pp = 0; pp < 8; ++pp) {
+        bool burn[2] = {false, false}, grow[2] = {false, false}, need[2];
+        int new_age[2] = {p.age_lo, p.age_lo};
 #pragma unroll
-        for (int d = 0; d < 8; ++d) {
-            const float* src = ps_base + (int64_t)d * HW + 4 * g4;
-            if (vec) {
-                const float4 v = *reinterpret_cast<const float4*>(src);
-                ps[d][0] = v.x; ps[d][1] = v.y; ps[d][2] = v.z; ps[d][3] = v.w;
+        for (int h = 0; h < 2; ++h) {
+            const int i = 2 * pp + h;
+            const bool ok = (okbits >> i) & 1u, is_tree = (treebits >> i) & 1u, is_empty = (emptybits >> i) & 1u;
+            const bool nb = (anyfire >> i) & 1u;
+            if (INJECT) {
+                need[h] = false;
+                burn[h] = (burnbits >> i) & 1u;
+                if (burn[h]) new_age[h] = inj_age[rowoff + i];
+                if (ok && is_empty) grow[h] = inj_grow[rowoff + i] < p.p_tree;
             } else {
+                need[h] = ok && ((is_tree && nb) || (is_empty && p.p_tree > 0.0f));
+            }
+        }
+        if (!INJECT) {
+            // Philox block for cell index pair lin>>1; word pair (2h, 2h+1) for h = lin & 1
+            const uint32_t linA = lin0 + (uint32_t)(2 * pp);
+            const uint32_t cA = linA >> 1, cB = (linA + 1u) >> 1;
+            u32x4 XA = u32x4{0u, 0u, 0u, 0u}, XB;
+            if (need[0] || (need[1] && cA == cB))
+                XA = philox4x32_10(u32x4{cA, env_id, step, GCA_TAG_ALEX_CELL}, k0, k1);
+            XB = XA;
+            if (need[1] && cA != cB) XB = philox4x32_10(u32x4{cB, env_id, step, GCA_TAG_ALEX_CELL}, k0, k1);
+            const bool hA = linA & 1u, hB = (linA + 1u) & 1u;
+            const uint32_t mains[2] = {hA ? XA.z : XA.x, hB ? XB.z : XB.x};
+            const uint32_t auxs[2] = {hA ? XA.w : XA.y, hB ? XB.w : XB.y};
 #pragma unroll
-                for (int j = 0; j < 4; ++j) ps[d][j] = (row_ok && cbase + 4 * g4 + j < W) ? src[j] : 0.0f;
+            for (int h = 0; h < 2; ++h) {
+                const int i = 2 * pp + h;
+                if (need[h]) {
+                    if ((treebits >> i) & 1u) {
+                        burn[h] = u01_f32(mains[h]) < __fsub_rn(1.0f, qn[i]);
+                        new_age[h] = randint_ms(auxs[h], p.age_lo, p.age_hi);
+                    } else {
+                        grow[h] = u01_f32(mains[h]) < p.p_tree;
+                    }
+                }
             }
         }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int i = 4 * g4 + j;
-            const bool ok = row_ok && cbase + i < W;
-            const int x = (int)((ownw[g4] >> (8 * j)) & 0xFFu);
-            const uint32_t nbm = (fm[g4] >> (8 * j)) & 0xFFu;
+        for (int h = 0; h < 2; ++h) {
+            const int i = 2 * pp + h;
+            const int x = (int)((own[i >> 2] >> (8 * (i & 3))) & 0xFFu);
             const int age = (int)(int16_t)(agew[i >> 1] >> (16 * (i & 1)));
-            // lookups with clip(idx, 1, 5) (:176-178) as select chains (no per-lane indexing)
-            const int vv = (int)((vgw[g4] >> (8 * j)) & 0xFFu), dd = (int)((dnw[g4] >> (8 * j)) & 0xFFu);
-            const float av = vv <= 1 ? p.veg1p[1] : vv == 2 ? p.veg1p[2] : vv == 3 ? p.veg1p[3] : vv == 4 ? p.veg1p[4] : p.veg1p[5];
-            const float ad = dd <= 1 ? p.den1p[1] : dd == 2 ? p.den1p[2] : dd == 3 ? p.den1p[3] : dd == 4 ? p.den1p[4] : p.den1p[5];
-            // p = p_h * (1 + p_veg) * (1 + p_den) * wind * p_slope, left to right (:206)
-            const float base = __fmul_rn(__fmul_rn(ph[i], av), ad);
-            if (want_prob && ok) {
-                float* po = prob_out + (rowoff + i) * 8;
-#pragma unroll
-                for (int d = 0; d < 8; ++d) po[d] = __fmul_rn(__fmul_rn(base, wind[d]), ps[d][j]);
-            }
             const bool is_tree = x == p.tree, is_empty = x == p.empty, is_fire = x == p.fire;
-            bool burn = false, grow = false;
-            int new_age_draw = p.age_lo;
-            if (INJECT) {
-                if (ok && is_tree && nbm) {
-                    const float* u = inj_burn + (rowoff + i) * 9;
-#pragma unroll
-                    for (int d = 0; d < 8; ++d) {
-                        const float pd = __fmul_rn(__fmul_rn(base, wind[d]), ps[d][j]);
-                        if (((nbm >> d) & 1u) && u[d < 4 ? d : d + 1] < pd) burn = true;
-                    }
-                    if (burn) new_age_draw = inj_age[rowoff + i];
-                }
-                if (ok && is_empty) grow = inj_grow[rowoff + i] < p.p_tree;
-            } else {
-                const bool need = ok && ((is_tree && nbm) || (is_empty && p.p_tree > 0.0f));
-                if (need) {
-                    const u32x4 rx =
-                        philox4x32_10(u32x4{(uint32_t)(r * W + cbase + i), env_id, step, GCA_TAG_ALEX_CELL}, k0, k1);
-                    if (is_tree) {
-                        float qn = 1.0f;
-#pragma unroll
-                        for (int d = 0; d < 8; ++d) {
-                            const float pd = __fmul_rn(__fmul_rn(base, wind[d]), ps[d][j]);
-                            if ((nbm >> d) & 1u) qn = __fmul_rn(qn, __fsub_rn(1.0f, clamp01(pd)));
-                        }
-                        burn = u01_f32(rx.x) < __fsub_rn(1.0f, qn);
-                        new_age_draw = randint_ms(rx.z, p.age_lo, p.age_hi);
-                    } else {
-                        grow = u01_f32(rx.y) < p.p_tree;
-                    }
-                }
-            }
             int nx = x;
-            if (is_tree && burn) nx = p.fire;
-            else if (is_empty && grow) nx = p.tree;
+            if (is_tree && burn[h]) nx = p.fire;
+            else if (is_empty && grow[h]) nx = p.tree;
             else if (is_fire && age <= 1) nx = p.empty;
-            int na = (nx == p.fire && !is_fire) ? new_age_draw : age;
+            int na = (nx == p.fire && !is_fire) ? new_age[h] : age;
             if (is_fire) na -= 1;
-            if (i & 1) nagew[i >> 1] |= (uint32_t)(uint16_t)na << 16;
-            else nagew[i >> 1] = (uint32_t)(uint16_t)na;
-            outw[g4] |= (uint32_t)(nx & 0xFF) << (8 * j);
-            if (ok) {
+            if (h) nagew[pp] |= (uint32_t)(uint16_t)na << 16;
+            else nagew[pp] = (uint32_t)(uint16_t)na;
+            outw[i >> 2] |= (uint32_t)(nx & 0xFF) << (8 * (i & 3));
+            if ((okbits >> i) & 1u) {
                 cntT += nx == p.tree;
                 cntF += nx == p.fire;
                 cntE += nx == p.empty;
             }
-        }    __builtin_amdgcn_sched_barrier(0);  // one group of 4 cells (8 x 16-B p_slope loads) in flight at a time
+        }
     }
 
     // ---------------- stores
     if (vec) {
-        *reinterpret_cast<uint4*>(grid_out + rowoff) = make_uint4(outw[0], outw[1], outw[2], outw[3]);
-        *reinterpret_cast<uint4*>(age_out + rowoff) = make_uint4(nagew[0], nagew[1], nagew[2], nagew[3]);
-        *reinterpret_cast<uint4*>(age_out + rowoff + 8) = make_uint4(nagew[4], nagew[5], nagew[6], nagew[7]);
+        uint8_t* gEo = grid_out + (size_t)e * HW;
+        int16_t* aEo = age_out + (size_t)e * HW;
+        *reinterpret_cast<uint4*>(gEo + lo) = make_uint4(outw[0], outw[1], outw[2], outw[3]);
+        *reinterpret_cast<uint4*>(aEo + lo) = make_uint4(nagew[0], nagew[1], nagew[2], nagew[3]);
+        *reinterpret_cast<uint4*>(aEo + lo + 8) = make_uint4(nagew[4], nagew[5], nagew[6], nagew[7]);
     } else if (row_ok) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
@@ -349,7 +441,7 @@ __global__ void alex_prepare_slope_kernel(const float* __restrict__ slope, float
     }
 }
 
-template <int R, bool INJ>
+template <int R, int MODE>
 void launch_alex(const gca_alex_params& p, int E, int H, int W, const uint8_t* gi, uint8_t* go, const int16_t* ai,
                  int16_t* ao, const uint8_t* veg, const uint8_t* den, const uint8_t* dous, const float* ps,
                  const int32_t* wi, const uint32_t* rs, const float* ib, const float* ig, const int32_t* ia, float* po,
@@ -357,18 +449,18 @@ void launch_alex(const gca_alex_params& p, int E, int H, int W, const uint8_t* g
     const int tiles_r = (H + TH - 1) / TH, tiles_c = (W + TW - 1) / TW;
     constexpr int RS = R < 2 ? 2 : R;
     constexpr int RR = TH + 2 * RS;
-    const size_t lds = sizeof(uint32_t) * (RR + 1) * CW + (size_t)RR * CW;
-    hipLaunchKernelGGL((alex_step_kernel<R, INJ>), dim3((unsigned)((int64_t)E * tiles_r * tiles_c)), dim3(256), lds, st,
+    const size_t lds = sizeof(uint32_t) * (RR + 1) * CWP + sizeof(uint16_t) * RR * (CW / 16);
+    hipLaunchKernelGGL((alex_step_kernel<R, MODE>), dim3((unsigned)((int64_t)E * tiles_r * tiles_c)), dim3(256), lds, st,
                        p, H, W, tiles_r, tiles_c, gi, go, ai, ao, veg, den, dous, ps, wi, rs, ib, ig, ia, po, counts);
 }
 
-template <bool INJ>
+template <int MODE>
 void dispatch_r(int R, const gca_alex_params& p, int E, int H, int W, const uint8_t* gi, uint8_t* go, const int16_t* ai,
                 int16_t* ao, const uint8_t* veg, const uint8_t* den, const uint8_t* dous, const float* ps,
                 const int32_t* wi, const uint32_t* rs, const float* ib, const float* ig, const int32_t* ia, float* po,
                 int32_t* counts, hipStream_t st) {
 #define GCA_ALEX_CASE(RV) \
-    case RV: launch_alex<RV, INJ>(p, E, H, W, gi, go, ai, ao, veg, den, dous, ps, wi, rs, ib, ig, ia, po, counts, st); break;
+    case RV: launch_alex<RV, MODE>(p, E, H, W, gi, go, ai, ao, veg, den, dous, ps, wi, rs, ib, ig, ia, po, counts, st); break;
     switch (R) {
         GCA_ALEX_CASE(1) GCA_ALEX_CASE(2) GCA_ALEX_CASE(3) GCA_ALEX_CASE(4)
         GCA_ALEX_CASE(5) GCA_ALEX_CASE(6) GCA_ALEX_CASE(7) GCA_ALEX_CASE(8)
@@ -407,11 +499,14 @@ extern "C" int gca_alex_step(const gca_alex_params* p, int E, int H, int W, cons
         return GCA_ERR_HIP;
     }
     if (inj)
-        dispatch_r<true>(p->R, *p, E, H, W, grid_in, grid_out, age_in, age_out, veg, den, dousing, p_slope, wind_index,
+        dispatch_r<2>(p->R, *p, E, H, W, grid_in, grid_out, age_in, age_out, veg, den, dousing, p_slope, wind_index,
                          rng_step, inj_burn, inj_grow, inj_age, prob_out, counts, st);
+    else if (prob_out)
+        dispatch_r<1>(p->R, *p, E, H, W, grid_in, grid_out, age_in, age_out, veg, den, dousing, p_slope, wind_index,
+                      rng_step, nullptr, nullptr, nullptr, prob_out, counts, st);
     else
-        dispatch_r<false>(p->R, *p, E, H, W, grid_in, grid_out, age_in, age_out, veg, den, dousing, p_slope, wind_index,
-                          rng_step, nullptr, nullptr, nullptr, prob_out, counts, st);
+        dispatch_r<0>(p->R, *p, E, H, W, grid_in, grid_out, age_in, age_out, veg, den, dousing, p_slope, wind_index,
+                      rng_step, nullptr, nullptr, nullptr, nullptr, counts, st);
     GCA_CHECK_LAUNCH("alex_step");
     return GCA_OK;
 }

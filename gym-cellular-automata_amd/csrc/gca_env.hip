@@ -56,15 +56,20 @@ __global__ void bulldozer_pre_kernel(gca_bulldozer_params p, const int32_t* __re
 __global__ void bulldozer_interpass_kernel(gca_bulldozer_params p, int pass, const int32_t* __restrict__ steps,
                                            uint8_t* __restrict__ parity, const double* __restrict__ wind,
                                            int64_t wind_stride, const uint32_t* __restrict__ rng_step,
-                                           uint8_t* __restrict__ dir_mask, int E) {
+                                           uint8_t* __restrict__ dir_mask, int32_t* __restrict__ counts, int E) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= E) return;
     const int n = steps[e];
     if (n > pass) parity[e] ^= 1;
-    if (n > pass + 1)
+    if (n > pass + 1) {
+        // the next pass recounts this env's new grid from zero
+        counts[3 * e + 0] = 0;
+        counts[3 * e + 1] = 0;
+        counts[3 * e + 2] = 0;
         dir_mask[e] = (uint8_t)windy_mask(wind + (int64_t)e * wind_stride, nullptr, (uint32_t)p.seed,
                                           (uint32_t)(p.seed >> 32), (uint32_t)(p.env_offset + e),
                                           rng_step[e] + (uint32_t)(pass + 1));
+    }
 }
 
 __global__ void bulldozer_post_kernel(gca_bulldozer_params p, int last_pass, const int32_t* __restrict__ action,
@@ -124,10 +129,11 @@ extern "C" int gca_bulldozer_pre(const gca_bulldozer_params* p, const int32_t* a
 
 extern "C" int gca_bulldozer_interpass(const gca_bulldozer_params* p, int pass, const int32_t* steps, uint8_t* parity,
                                        const double* wind, int64_t wind_stride, const uint32_t* rng_step,
-                                       uint8_t* dir_mask, int E, void* stream) {
-    GCA_CHECK_ARG(p && steps && parity && wind && rng_step && dir_mask && E > 0, "bulldozer_interpass: null argument");
+                                       uint8_t* dir_mask, int32_t* counts, int E, void* stream) {
+    GCA_CHECK_ARG(p && steps && parity && wind && rng_step && dir_mask && counts && E > 0,
+                  "bulldozer_interpass: null argument");
     hipLaunchKernelGGL(bulldozer_interpass_kernel, ENV_GRID(E), 0, (hipStream_t)stream, *p, pass, steps, parity, wind,
-                       wind_stride, rng_step, dir_mask, E);
+                       wind_stride, rng_step, dir_mask, counts, E);
     GCA_CHECK_LAUNCH("bulldozer_interpass");
     return GCA_OK;
 }

@@ -97,7 +97,7 @@ _SIGNATURES = {
     "gca_windy_dirmask": ([P, c_int64, P, c_uint64, P, P, c_int, c_int, P, c_int, P], c_int),
     "gca_windy_step": ([P, P, P, P, c_int, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, P], c_int),
     "gca_bulldozer_pre": ([POINTER(BulldozerParams), P, P, P, P, P, c_int64, P, P, P, c_int, P], c_int),
-    "gca_bulldozer_interpass": ([POINTER(BulldozerParams), c_int, P, P, P, c_int64, P, P, c_int, P], c_int),
+    "gca_bulldozer_interpass": ([POINTER(BulldozerParams), c_int, P, P, P, c_int64, P, P, P, c_int, P], c_int),
     "gca_bulldozer_post": ([POINTER(BulldozerParams), c_int, P, P, P, P, P, c_int, c_int, P, P, P, P, P, P, c_int, P],
                            c_int),
     "gca_move_modify": ([POINTER(BulldozerParams), P, P, P, c_int, c_int, P, c_int, P], c_int),

@@ -135,7 +135,8 @@ class BatchedForestFireBulldozerEnv:
                  dev.ptr(self.counts), st)
             if pss < P - 1:
                 call("gca_bulldozer_interpass", p, pss, dev.ptr(self.steps), dev.ptr(self.parity),
-                     dev.ptr(self.wind), 9, dev.ptr(self.rng_step), dev.ptr(self.dir_mask), E, st)
+                     dev.ptr(self.wind), 9, dev.ptr(self.rng_step), dev.ptr(self.dir_mask), dev.ptr(self.counts), E,
+                     st)
         call("gca_bulldozer_post", p, P - 1, dev.ptr(a), dev.ptr(self.steps), dev.ptr(self.parity),
              dev.ptr(self.buf[0]), dev.ptr(self.buf[1]), H, W, dev.ptr(self.pos), dev.ptr(self.counts),
              dev.ptr(self.rng_step), dev.ptr(self.done), dev.ptr(self.hit), dev.ptr(self.reward), E, st)

@@ -96,11 +96,11 @@ typedef struct {
 int gca_bulldozer_pre(const gca_bulldozer_params* p, const int32_t* action, double* accu, int32_t* steps,
                       const uint8_t* done, const double* wind, int64_t wind_stride, const uint32_t* rng_step,
                       uint8_t* dir_mask, int32_t* counts, int E, void* stream);
-/* Between CA passes `pass` and `pass+1`: flip parity of envs that stepped in `pass`
- * and draw the dir_mask for pass+1.                                             */
+/* Between CA passes `pass` and `pass+1`: flip parity of envs that stepped in `pass`;
+ * for envs stepping again, zero their counts and draw the dir_mask for pass+1.  */
 int gca_bulldozer_interpass(const gca_bulldozer_params* p, int pass, const int32_t* steps, uint8_t* parity,
                             const double* wind, int64_t wind_stride, const uint32_t* rng_step, uint8_t* dir_mask,
-                            int E, void* stream);
+                            int32_t* counts, int E, void* stream);
 /* After the last pass (index last_pass): flip parity, Move, Modify (in place on the
  * current buffer), adjust counts, reward = -(f/(t+f)) (NaN if t+f==0), done = (f==0),
  * rng_step += steps. Done-on-entry envs: reward 0, nothing moves.                  */

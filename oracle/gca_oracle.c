@@ -14,7 +14,8 @@
  *   p_h   = heat - dous                      (:198)
  *   p_d   = ((((p_h * av) * ad) * wind[d]) * p_slope[d])                       (:206)
  *   injected: TREE -> FIRE iff exists fire neighbour d with u[d] < p_d (:379-383)
- *   philox  : TREE -> FIRE iff u0 < 1 - prod_{fire d} (1 - clamp01(p_d))
+ *   philox  : TREE -> FIRE iff u(main) < 1 - prod_{fire d} (1 - clamp01(p_d)), where the cell with
+ *             index lin uses words (2h, 2h+1), h = lin & 1, of Philox(lin >> 1, env, step, ALXC)
  *   EMPTY -> TREE iff u < p_tree; FIRE -> EMPTY iff age <= 1; ages (:394-423).
  */
 #include <math.h>
@@ -165,17 +166,20 @@ static void alex_env(const oracle_alex_params* p, int e, int H, int W, const uin
                 }
                 if (is_empty) grow = ig[cell] < p->p_tree;
             } else if ((is_tree && fm) || (is_empty && p->p_tree > 0.0f)) {
-                const uint32_t ctr[4] = {(uint32_t)cell, env_id, step, TAG_ALEX_CELL};
+                /* one Philox block per cell pair: counter lin >> 1, words (2h, 2h+1) for h = lin & 1 */
+                const uint32_t ctr[4] = {(uint32_t)cell >> 1, env_id, step, TAG_ALEX_CELL};
                 uint32_t rx[4];
                 philox(ctr, k0, k1, rx);
+                const int h = (int)(cell & 1);
+                const uint32_t main_w = rx[2 * h], aux_w = rx[2 * h + 1];
                 if (is_tree) {
                     float qn = 1.0f;
                     for (int q = 0; q < 8; ++q)
                         if ((fm >> q) & 1u) qn = qn * (1.0f - clamp01(pd[q]));
-                    burn = u01(rx[0]) < 1.0f - qn;
-                    new_age = randint_ms(rx[2], p->age_lo, p->age_hi);
+                    burn = u01(main_w) < 1.0f - qn;
+                    new_age = randint_ms(aux_w, p->age_lo, p->age_hi);
                 } else {
-                    grow = u01(rx[1]) < p->p_tree;
+                    grow = u01(main_w) < p->p_tree;
                 }
             }
             int nx = x;

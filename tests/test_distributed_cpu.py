@@ -1,0 +1,81 @@
+"""Multi-process path on CPU (gloo, world_size 2) and the sharding convention."""
+import os
+import socket
+
+import numpy as np
+import torch
+import torch.multiprocessing as mp
+
+from gymca_amd.distributed import all_gather_stats, shard
+from oracle import windy as owindy
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    off, n = shard(7, world, rank)
+    done = torch.tensor([(off + i) % 2 for i in range(n)], dtype=torch.uint8)
+    ret = torch.tensor([-(off + i) / 10 for i in range(n)], dtype=torch.float32)
+    ln = torch.tensor([off + i for i in range(n)], dtype=torch.int32)
+    # uneven shards are padded to the largest shard before gathering
+    E = max(shard(7, world, r)[1] for r in range(world))
+    pad = E - n
+    d, r, l = all_gather_stats(torch.cat([done, torch.zeros(pad, dtype=torch.uint8)]),
+                               torch.cat([ret, torch.zeros(pad)]), torch.cat([ln, torch.zeros(pad, dtype=torch.int32)]))
+    q.put((rank, d.tolist(), r.tolist(), l.tolist()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_shard_covers_all_envs():
+    for n in (1, 7, 8, 4096, 8191):
+        for w in (1, 2, 3, 8):
+            spans = [shard(n, w, r) for r in range(w)]
+            assert spans[0][0] == 0 and sum(c for _, c in spans) == n
+            assert all(spans[i][0] + spans[i][1] == spans[i + 1][0] for i in range(w - 1))
+
+
+def test_gloo_world2_all_gather_of_episode_stats():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res = {r: (d, ret, ln) for r, d, ret, ln in out}
+    assert res[0] == res[1]
+    d, ret, ln = res[0]
+    # rank 0 holds envs 0..3, rank 1 holds 4..6 (+1 pad)
+    assert ln[:4] == [0, 1, 2, 3] and ln[4:7] == [4, 5, 6]
+    assert d[:4] == [0, 1, 0, 1] and np.allclose(ret[4:7], [-0.4, -0.5, -0.6])
+
+
+def test_sharded_philox_streams_equal_unsharded():
+    """Global env ids in every counter: two shards reproduce the single-shard trajectories."""
+    rng = np.random.default_rng(0)
+    E, N = 4, 24
+    grids = [rng.choice([0, 3, 25], size=(N, N), p=[0.1, 0.7, 0.2]) for _ in range(E)]
+    pos = [(6, 18)] * E
+    wind = np.full((3, 3), 0.6)
+    full = owindy.BulldozerOracle(grids, pos, wind, 0.6, 0.3, 0.001, seed=11)
+    a = owindy.BulldozerOracle(grids[:2], pos[:2], wind, 0.6, 0.3, 0.001, seed=11, env_offset=0)
+    b = owindy.BulldozerOracle(grids[2:], pos[2:], wind, 0.6, 0.3, 0.001, seed=11, env_offset=2)
+    for s in range(30):
+        act = np.stack([rng.integers(0, 9, E), rng.integers(0, 2, E)], axis=1)
+        full.step(act)
+        a.step(act[:2])
+        b.step(act[2:])
+    for e in range(E):
+        assert np.array_equal(full.grids[e], (a.grids + b.grids)[e])
