@@ -11,15 +11,19 @@
 //
 // Mapping (one workgroup = 256 threads = TH x TW = 16 x 256 cells of one env):
 //   thread (tr = tid/16, q = tid%16) owns 16 consecutive cells of one row -> 16-B loads.
-//   LDS: the grid rows [r0-R, r0+TH+R) x cols [c0-16, c0+TW+16) staged once, and the
-//   column-prefix CP of packed v = fire | dousing<<16 (u32). Box sums of radius k are
-//   sum over 16+2k columns of (CP[row+k+1] - CP[row-k]) with a sliding window; fire and
-//   dousing fields never interfere because every box sum of either field is < 2^16.
-//   Ring counts n_k = B_k - B_{k-1} are exact integers; heat is then
-//   ((w0*n0 + w1*n1) + w2*n2) + ...  in f32 (fixed order, no fma): deterministic.
+//   LDS: the grid rows [r0-R, r0+TH+R) x cols [c0-16, c0+TW+16) staged once as the
+//   column prefix CP of packed v = fire | dousing<<16 (u32; v_perm_b32 builds each word) plus
+//   a FIRE bitmask FB. Box sums B_k of radius k = sliding window over 16+2k columns of
+//   (CP[row+k+1] - CP[row-k]); fire and dousing fields never interfere (box sums < 2^16).
+//   heat = sum_k dw_k * B_k in f32 (fixed order, separately rounded, packed over cell pairs).
+// Lane work: per-cell decisions are single compares; the state update, output bytes (v_perm),
+//   ages (SWAR i16 pairs) and counts (popcount) are word-level operations on 16-bit cell masks.
+// p_slope (78% of the bytes) streams through a depth-2 register pipeline: direction d+2 is in
+//   flight while direction d+1 is consumed; direction 0 rides with the staging loads.
 // Draws: INJECT = the reference's own uniform/randint arrays (exact rule);
-//        Philox = one Philox4x32-10 block per cell that needs it: x0 burn, x1 grow, x2 age;
-//        burn iff u0 < 1 - prod_{fire d}(1 - clamp01(p_d)) (same law as independent draws).
+//        Philox = one Philox4x32-10 block per cell pair: words (main, aux) per cell;
+//        burn iff u(main) < 1 - prod_{fire d}(1 - clamp01(p_d)) (same law as independent draws),
+//        grow iff u(main) < p_tree, new fire age = randint(aux).
 #include "gca_common.h"
 
 namespace {
@@ -34,11 +38,47 @@ constexpr int CWP = 336;
 __host__ __device__ constexpr int pcol(int c) { return c + (c >> 4); }
 static_assert(pcol(CW - 1) < CWP && CWP % 32 == 16, "padded row");
 
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+typedef int16_t i16x2 __attribute__((ext_vector_type(2)));
+
 __device__ __forceinline__ float clamp01(float v) { return fminf(fmaxf(v, 0.0f), 1.0f); }
+// clamp01(a * b) on both halves: one v_pk_mul_f32 with the clamp output modifier; the product is
+// rounded first, then clamped (= clamp01(__fmul_rn(a, b)), NaN -> 0 like fminf(fmaxf(NaN, 0), 1))
+__device__ __forceinline__ f2 pk_mul_clamp01(f2 a, f2 b) {
+    f2 r;
+    asm("v_pk_mul_f32 %0, %1, %2 clamp" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+// bits = 2 * bits + (a < b): v_cmp into VCC + add-with-carry (cell 0 lands in the top bit; reversed later)
+__device__ __forceinline__ uint32_t push_lt(uint32_t bits, float a, float b) {
+    asm("v_cmp_lt_f32 vcc, %1, %2\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc" : "+v"(bits) : "v"(a), "v"(b) : "vcc");
+    return bits;
+}
+// 4-bit mask of the bytes of x equal to the byte of pat (bit j <-> byte j)
+__device__ __forceinline__ uint32_t eq_nib(uint32_t x, uint32_t pat) { return (bytes_eq01(x, pat) * 0x01020408u) >> 24; }
+// nibble (bit j) -> 0x01 in byte j; the four partial products never overlap
+__device__ __forceinline__ uint32_t spread4(uint32_t n) { return ((n & 0xFu) * 0x00204081u) & 0x01010101u; }
+__device__ __forceinline__ uint32_t bfi32(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
+// bit i of w as an all-ones / all-zeros word (v_bfe_i32)
+__device__ __forceinline__ uint32_t sbit(uint32_t w, int i) { return (uint32_t)((int32_t)(w << (31 - i)) >> 31); }
+template <class T, class S> __device__ __forceinline__ T bitcast_(S s) {
+    static_assert(sizeof(T) == sizeof(S), "size");
+    T t;
+    __builtin_memcpy(&t, &s, sizeof(T));
+    return t;
+}
 
 // MODE: 0 = Philox draws (production), 1 = Philox + debug burn probabilities, 2 = injected draws
 // (+ probabilities when prob_out != NULL). The debug store is compiled out of mode 0.
-template <int R, int MODE>
+//
+// Lane work is organised around 16-bit cell masks (bit i <-> the lane's cell i) and packed f32 pairs:
+// per-cell decisions are single compares; the state update, the output bytes, the ages and the counts
+// are word-level bit operations (see the rule section). Every f32 op keeps the oracle's order and
+// rounding (packed ops round each half like the scalar op; -ffp-contract=off).
+// FAST: W % TW == 0, H % TH == 0, every array 16-B aligned (checked on the host): all per-lane bounds
+// checks and byte-wise fallbacks compile away, which also lets the waitcnt pass keep loads in flight.
+template <int R, int MODE, bool FAST>
 __global__ __launch_bounds__(256, 4) void alex_step_kernel(
     gca_alex_params p, int H, int W, int tiles_r, int tiles_c, const uint8_t* __restrict__ grid_in,
     uint8_t* __restrict__ grid_out, const int16_t* __restrict__ age_in, int16_t* __restrict__ age_out,
@@ -52,8 +92,10 @@ __global__ __launch_bounds__(256, 4) void alex_step_kernel(
     constexpr int RR = TH + 2 * RS;    // staged rows
     constexpr int NCH = CW / 16;       // 16-column chunks per staged row
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    uint32_t* CP = reinterpret_cast<uint32_t*>(smem);                             // [RR+1][CWP] column prefix
-    uint16_t* FB = reinterpret_cast<uint16_t*>(smem + sizeof(uint32_t) * (RR + 1) * CWP);  // [RR][NCH] fire bits
+    uint32_t* CP = reinterpret_cast<uint32_t*>(smem);                                        // [RR+1][CWP]
+    uint16_t* FB = reinterpret_cast<uint16_t*>(smem + sizeof(uint32_t) * (RR + 1) * CWP);   // [RR][NCH] fire bits
+    float* LUT = reinterpret_cast<float*>(smem + sizeof(uint32_t) * (RR + 1) * CWP + sizeof(uint16_t) * RR * NCH);
+    // LUT[0..7] = 1 + p_veg[clip(v, 1, 5)] for v = min(byte, 7); LUT[8..15] the same for density
 
     // XCD-aware order: blocks b, b+8, b+16, ... share an XCD (and its L2) under round-robin
     // dispatch; give each XCD a contiguous range of (env, tile) so the halo rows a tile stages
@@ -70,17 +112,17 @@ __global__ __launch_bounds__(256, 4) void alex_step_kernel(
     const uint8_t* gE = grid_in + (int64_t)e * HW;
     const uint8_t* dE = dousing + (int64_t)e * HW;
     const int tid = threadIdx.x;
-    const bool rows16 = ((W & 15) == 0) &&
+    const bool rows16 = FAST || ((W & 15) == 0) &&
                         ((((uintptr_t)grid_in) | ((uintptr_t)dousing) | ((uintptr_t)grid_out) | ((uintptr_t)veg) |
                           ((uintptr_t)den) | ((uintptr_t)age_in) | ((uintptr_t)age_out) | ((uintptr_t)p_slope)) &
                          15u) == 0;
-    const uint32_t Fp = rep4((uint32_t)p.fire), Ep = rep4((uint32_t)p.empty);
+    const uint32_t Fp = rep4((uint32_t)p.fire), Ep = rep4((uint32_t)p.empty), Tp = rep4((uint32_t)p.tree);
 
     // ---------------- this thread's 16 cells: row r, columns [cbase, cbase+16)
     const int tr = tid >> 4, q = tid & 15;
     const int r = r0 + tr;
     const int cbase = c0 + 16 * q;
-    const bool row_ok = r < H;
+    const bool row_ok = FAST || r < H;
     const int rr = RS + tr;  // staged row of r
     // global addressing: wave-uniform per-env base pointers (SGPRs) + 32-bit lane offsets,
     // so no 64-bit address VGPRs stay live across the kernel
@@ -90,7 +132,9 @@ __global__ __launch_bounds__(256, 4) void alex_step_kernel(
     const uint8_t* vE = veg + (size_t)e * HW;
     const uint8_t* nE = den + (size_t)e * HW;
     const int64_t rowoff = (int64_t)e * HW + lo;  // debug / injected arrays only
-    const bool vec = row_ok && rows16 && (cbase + 16 <= W);
+    const bool vec = FAST || (row_ok && rows16 && (cbase + 16 <= W));
+    const int nvalid = row_ok ? min(16, W - cbase) : 0;
+    const uint32_t okB = FAST ? 0xFFFFu : nvalid >= 16 ? 0xFFFFu : (nvalid > 0 ? (1u << nvalid) - 1u : 0u);
 
     // per-cell inputs, issued before the LDS phases so their latency overlaps them
     // (fire ages are loaded later, after the direction pass, to keep them out of its VGPR peak)
@@ -119,19 +163,67 @@ __global__ __launch_bounds__(256, 4) void alex_step_kernel(
         }
     }
 
+    // ---- p_slope software pipeline (depth 2): direction 0 is issued with the staging loads,
+    //      direction 1 right after the heat phase, so their HBM latency overlaps the heat computation; direction
+    //      d+2 is issued as soon as d is consumed.
+    //      p_slope is 78% of the kernel's bytes, so keeping two directions in flight per wave is what
+    //      keeps HBM busy while the waves compute.
+    const float* psE = p_slope + (size_t)e * 8 * HW;  // wave-uniform
+    auto load_ps = [&](int d, float4 (&v)[4]) {
+        const float* src = psE + (uint32_t)(d * (uint32_t)HW) + lo;
+        if (vec) {
+#pragma unroll
+            for (int m = 0; m < 4; ++m) v[m] = *reinterpret_cast<const float4*>(src + 4 * m);
+        } else {
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                float t4[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) t4[j] = (row_ok && cbase + 4 * m + j < W) ? src[4 * m + j] : 0.0f;
+                v[m] = make_float4(t4[0], t4[1], t4[2], t4[3]);
+            }
+        }
+    };
+    float4 psbuf[2][4];
+    uint32_t agew[8];
+    auto load_ages = [&]() {
+        if (vec) {
+            const uint4 a0 = *reinterpret_cast<const uint4*>(aEi + lo);
+            const uint4 a1 = *reinterpret_cast<const uint4*>(aEi + lo + 8);
+            agew[0] = a0.x; agew[1] = a0.y; agew[2] = a0.z; agew[3] = a0.w;
+            agew[4] = a1.x; agew[5] = a1.y; agew[6] = a1.z; agew[7] = a1.w;
+        } else {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) agew[k] = 0u;
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+                if (row_ok && cbase + i < W) agew[i >> 1] |= (uint32_t)(uint16_t)aEi[lo + i] << (16 * (i & 1));
+        }
+    };
     // ---------------- stage rows [r0-RS, r0+TH+RS) x cols [c0-16, c0+TW+16):
     //                  packed fire | dousing<<16 -> CP rows 1..RR, fire bitmask -> FB
-    for (int ch = tid; ch < RR * NCH; ch += 256) {
+    //                  every load of the thread's chunks is issued before any is processed
+    constexpr int NIT = (RR * NCH + 255) / 256;
+    uint32_t sgw[NIT][4], sdw[NIT][4];
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+        const int ch = tid + 256 * it;
         const int sr = ch / NCH, cq = ch - sr * NCH;
         const int gr = r0 - RS + sr, gc = c0 - 16 + 16 * cq;
-        uint32_t gw[4] = {Ep, Ep, Ep, Ep}, dw[4] = {0u, 0u, 0u, 0u};
-        if (gr >= 0 && gr < H) {
-            if (rows16 && gc >= 0 && gc + 16 <= W) {
+        uint32_t* gw = sgw[it];
+        uint32_t* dw = sdw[it];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            gw[j] = Ep;
+            dw[j] = 0u;
+        }
+        if (ch < RR * NCH && gr >= 0 && gr < H) {
+            if (rows16 && gc >= 0 && gc + 16 <= W) {  // FAST: a chunk is entirely inside or outside
                 const uint4 a = *reinterpret_cast<const uint4*>(gE + (int64_t)gr * W + gc);
                 const uint4 b = *reinterpret_cast<const uint4*>(dE + (int64_t)gr * W + gc);
                 gw[0] = a.x; gw[1] = a.y; gw[2] = a.z; gw[3] = a.w;
                 dw[0] = b.x; dw[1] = b.y; dw[2] = b.z; dw[3] = b.w;
-            } else {
+            } else if (!FAST) {
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
                     const int c = gc + i;
@@ -143,20 +235,35 @@ __global__ __launch_bounds__(256, 4) void alex_step_kernel(
                 }
             }
         }
+    }
+    load_ps(0, psbuf[0]);  // first p_slope direction rides along with the staging loads
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+        const int ch = tid + 256 * it;
+        if (ch >= RR * NCH) break;
+        const int sr = ch / NCH, cq = ch - sr * NCH;
         uint32_t* cp = CP + (sr + 1) * CWP + 17 * cq;  // = pcol(16 * cq)
         uint32_t bits = 0u;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const uint32_t f = bytes_eq01(gw[j], Fp);
-            bits |= ((f & 1u) | ((f >> 7) & 2u) | ((f >> 14) & 4u) | ((f >> 21) & 8u)) << (4 * j);
-            cp[4 * j + 0] = (f & 1u) | ((dw[j] & 0xFFu) << 16);
-            cp[4 * j + 1] = ((f >> 8) & 1u) | (((dw[j] >> 8) & 0xFFu) << 16);
-            cp[4 * j + 2] = ((f >> 16) & 1u) | (((dw[j] >> 16) & 0xFFu) << 16);
-            cp[4 * j + 3] = ((f >> 24) & 1u) | (((dw[j] >> 24) & 0xFFu) << 16);
+            const uint32_t f = bytes_eq01(sgw[it][j], Fp);  // 0x01 in every FIRE byte
+            bits |= ((f * 0x01020408u) >> 24) << (4 * j);
+            // cell m of this word: (fire flag) | (dousing byte) << 16, one v_perm_b32 each
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+                cp[4 * j + m] =
+                    __builtin_amdgcn_perm(sdw[it][j], f, 0x0C000C00u | ((4u + (uint32_t)m) << 16) | (uint32_t)m);
         }
         FB[sr * NCH + cq] = (uint16_t)bits;
     }
     for (int cc = tid; cc < CWP; cc += 256) CP[cc] = 0u;
+    if (tid < 16) {
+        const int v = tid & 7;
+        // selects on the (SGPR) kernel arguments only: no dynamic indexing into the argument struct
+        const float av = v <= 1 ? p.veg1p[1] : v == 2 ? p.veg1p[2] : v == 3 ? p.veg1p[3] : v == 4 ? p.veg1p[4] : p.veg1p[5];
+        const float ad = v <= 1 ? p.den1p[1] : v == 2 ? p.den1p[2] : v == 3 ? p.den1p[3] : v == 4 ? p.den1p[4] : p.den1p[5];
+        LUT[tid] = tid < 8 ? av : ad;
+    }
     __syncthreads();
     // ---------------- column prefix: columns t and t + CW/2 per thread, every load before the adds
     if (tid < CW / 2) {
@@ -178,17 +285,21 @@ __global__ __launch_bounds__(256, 4) void alex_step_kernel(
     }
     __syncthreads();
 
+    __builtin_amdgcn_sched_barrier(0);
+
     // ---- heat and dousing from box sums B_k (fire field) and D_1, D_2 (dousing field):
     //   heat = sum_k n_k*w_k = sum_{k=0..R} B_k * dw_k   (dw_k = w_k - w_{k+1}, w_{R+1} = 0: p.heat_dw)
     //   dous = inner*D_1 + border*(D_2 - D_1) = (inner - border)*D_1 + border*D_2
     // Fixed evaluation order, every op separately rounded: bit-identical with the C oracle.
-    float ph[16], dz[16];
+    // Pairs of cells share one packed mul / add; B_k <= (2R+1)^2 <= 225 for R <= 7 -> v_cvt_f32_ubyte0.
+    f2 ph2[8], dz2[8];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        ph[i] = 0.0f;
-        dz[i] = 0.0f;
+    for (int j = 0; j < 8; ++j) {
+        ph2[j] = (f2){0.0f, 0.0f};
+        dz2[j] = (f2){0.0f, 0.0f};
     }
     const float w_in_minus_bd = __fsub_rn(p.dous_inner, p.dous_border);
+    auto fire_f = [](uint32_t s) -> float { return R <= 7 ? (float)(s & 0xFFu) : (float)(s & 0xFFFFu); };
 #pragma unroll
     for (int k = 0; k <= RS; ++k) {
         uint32_t V[16 + 2 * RS];
@@ -203,7 +314,7 @@ __global__ __launch_bounds__(256, 4) void alex_step_kernel(
             }
             if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);  // <= 16 LDS reads in flight (VGPR budget)
         }
-        uint32_t s = 0u;
+        uint32_t s = 0u, sprev = 0u;
 #pragma unroll
         for (int j = 0; j <= 2 * RS; ++j)
             if (j <= 2 * k) s += V[j];
@@ -211,18 +322,24 @@ __global__ __launch_bounds__(256, 4) void alex_step_kernel(
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
             if (i > 0) s += V[i + 2 * k] - V[i - 1];
-            if (k <= R) ph[i] = __fadd_rn(ph[i], __fmul_rn(wk, (float)(s & 0xFFFFu)));
-            if (k == 1) dz[i] = __fmul_rn(w_in_minus_bd, (float)(s >> 16));
-            if (k == 2) dz[i] = __fadd_rn(dz[i], __fmul_rn(p.dous_border, (float)(s >> 16)));
+            if (i & 1) {
+                const int j = i >> 1;
+                if (k <= R) ph2[j] = ph2[j] + (f2){wk, wk} * (f2){fire_f(sprev), fire_f(s)};
+                const f2 dsum = {(float)(sprev >> 16), (float)(s >> 16)};
+                if (k == 1) dz2[j] = (f2){w_in_minus_bd, w_in_minus_bd} * dsum;
+                if (k == 2) dz2[j] = dz2[j] + (f2){p.dous_border, p.dous_border} * dsum;
+            }
+            sprev = s;
         }
         // materialise this radius' partial sums now: without it hipcc keeps all (R+1)x16 window
         // sums live and evaluates the f32 chains at the end (-> spills at R >= 4)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) asm volatile("" : "+v"(ph[i]), "+v"(dz[i]));
+        for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(ph2[j]), "+v"(dz2[j]));
         __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
-    for (int i = 0; i < 16; ++i) ph[i] = __fsub_rn(ph[i], dz[i]);  // p_h = heat - dousing (:198)
+    for (int j = 0; j < 8; ++j) ph2[j] = ph2[j] - dz2[j];  // p_h = heat - dousing (:198)
+    load_ps(1, psbuf[1]);
 
     // ---- FIRE bits of rows r-1, r, r+1: bit j of nbw[a] <-> staged column cc0 - 1 + j (j = 0..17)
     uint32_t nbw[3];
@@ -243,19 +360,26 @@ __global__ __launch_bounds__(256, 4) void alex_step_kernel(
     const bool want_prob = PROB && prob_out != nullptr;
     const uint32_t lin0 = lo;  // cell index of cell 0 within the env
 
-    // ---- base[i] = (p_h * (1 + p_veg)) * (1 + p_den)   (left-to-right product of :206)
-    uint32_t treebits = 0u, emptybits = 0u, okbits = 0u;
+    // ---- cell-state masks of the lane's 16 cells
+    uint32_t treeB = 0u, emptyB = 0u;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const int x = (int)((own[i >> 2] >> (8 * (i & 3))) & 0xFFu);
-        treebits |= (uint32_t)(x == p.tree) << i;
-        emptybits |= (uint32_t)(x == p.empty) << i;
-        okbits |= (uint32_t)(row_ok && cbase + i < W) << i;
-        // lookups with clip(idx, 1, 5) (:176-178) as select chains (no per-lane indexing)
-        const int vv = (int)((vgw[i >> 2] >> (8 * (i & 3))) & 0xFFu), dd = (int)((dnw[i >> 2] >> (8 * (i & 3))) & 0xFFu);
-        const float av = vv <= 1 ? p.veg1p[1] : vv == 2 ? p.veg1p[2] : vv == 3 ? p.veg1p[3] : vv == 4 ? p.veg1p[4] : p.veg1p[5];
-        const float ad = dd <= 1 ? p.den1p[1] : dd == 2 ? p.den1p[2] : dd == 3 ? p.den1p[3] : dd == 4 ? p.den1p[4] : p.den1p[5];
-        ph[i] = __fmul_rn(__fmul_rn(ph[i], av), ad);  // ph now holds base
+    for (int j = 0; j < 4; ++j) {
+        treeB |= eq_nib(own[j], Tp) << (4 * j);
+        emptyB |= eq_nib(own[j], Ep) << (4 * j);
+    }
+    const uint32_t fireB = (nbw[1] >> 1) & 0xFFFFu;
+
+    // ---- base = (p_h * (1 + p_veg)) * (1 + p_den)   (left-to-right product of :206), clip(idx, 1, 5)
+    //      (:176-178) through the LDS table
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int i0 = 2 * j, i1 = 2 * j + 1;
+        const uint32_t v0 = min((vgw[i0 >> 2] >> (8 * (i0 & 3))) & 0xFFu, 7u);
+        const uint32_t v1 = min((vgw[i1 >> 2] >> (8 * (i1 & 3))) & 0xFFu, 7u);
+        const uint32_t d0 = min((dnw[i0 >> 2] >> (8 * (i0 & 3))) & 0xFFu, 7u);
+        const uint32_t d1 = min((dnw[i1 >> 2] >> (8 * (i1 & 3))) & 0xFFu, 7u);
+        const f2 av = {LUT[v0], LUT[v1]}, ad = {LUT[8 + d0], LUT[8 + d1]};
+        ph2[j] = (ph2[j] * av) * ad;  // ph2 now holds base
     }
     // burning-neighbour mask of direction d for all 16 cells: bit i <-> cell i
     // d = (a, b) row-major without the centre; entry (a, b) = cell (r + a - 1, c + b - 1) (:332-337)
@@ -269,130 +393,143 @@ __global__ __launch_bounds__(256, 4) void alex_step_kernel(
     for (int d = 0; d < 8; ++d) anyfire |= dir_bits(d);
 
     // ---- direction-outer pass: each p_slope row segment (16 floats = 64 B per lane, 1 KiB per
-    //      16 lanes) is read in one burst, so every HBM line is consumed by one wave instruction group
-    float qn[16];
+    //      16 lanes) is read in one burst, so every HBM line is consumed by one wave instruction group.
+    //      qn = prod over burning directions of (1 - clamp01(p_d)); a non-burning direction multiplies
+    //      by exactly 1.0f (bit-select), so the product equals the oracle's skip-form.
+    f2 qn2[8];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) qn[i] = 1.0f;
-    uint32_t burnbits = 0u;
-    const float* psE = p_slope + (size_t)e * 8 * HW;  // wave-uniform
-    auto load_ps = [&](int d, float4 (&v)[4]) {
-        const float* src = psE + (uint32_t)(d * (uint32_t)HW) + lo;
-        if (vec) {
-#pragma unroll
-            for (int m = 0; m < 4; ++m) v[m] = *reinterpret_cast<const float4*>(src + 4 * m);
-        } else {
-#pragma unroll
-            for (int m = 0; m < 4; ++m) {
-                float t4[4];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) t4[j] = (row_ok && cbase + 4 * m + j < W) ? src[4 * m + j] : 0.0f;
-                v[m] = make_float4(t4[0], t4[1], t4[2], t4[3]);
-            }
-        }
-    };
+    for (int j = 0; j < 8; ++j) qn2[j] = (f2){1.0f, 1.0f};
+    uint32_t burn_inj = 0u;
 #pragma unroll
     for (int d = 0; d < 8; ++d) {
-        float4 psc[4];
-        load_ps(d, psc);
-        const uint32_t fb = dir_bits(d) & treebits & okbits;
-        const float wd = wind[d];
+        float4 (&psc)[4] = psbuf[d & 1];
+        // pin base here: otherwise the 64 direction-independent products base*wind[d] are hoisted
+        // above the loop (128 live VGPRs -> spills)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const float4 v4 = psc[i >> 2];
-            const float ps = (i & 3) == 0 ? v4.x : (i & 3) == 1 ? v4.y : (i & 3) == 2 ? v4.z : v4.w;
-            const float pd = __fmul_rn(__fmul_rn(ph[i], wd), ps);
-            if (PROB && want_prob && ((okbits >> i) & 1u)) prob_out[(rowoff + i) * 8 + d] = pd;
-            const bool f = (fb >> i) & 1u;
-            if (INJECT) {
-                if (f && inj_burn[(rowoff + i) * 9 + (d < 4 ? d : d + 1)] < pd) burnbits |= 1u << i;
+        for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(ph2[j]));
+        // qn of non-tree / out-of-range cells is never used (burn is masked by treeB & okB)
+        const uint32_t fbd = INJECT ? (dir_bits(d) & treeB & okB) : dir_bits(d);
+        const f2 wd2 = {wind[d], wind[d]};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float4 v4 = psc[j >> 1];
+            const f2 ps = (j & 1) ? (f2){v4.z, v4.w} : (f2){v4.x, v4.y};
+            const f2 t = ph2[j] * wd2;
+            f2 c;
+            if (PROB) {
+                const f2 pd = t * ps;
+                if (want_prob) {
+                    if ((okB >> (2 * j)) & 1u) prob_out[(rowoff + 2 * j) * 8 + d] = pd.x;
+                    if ((okB >> (2 * j + 1)) & 1u) prob_out[(rowoff + 2 * j + 1) * 8 + d] = pd.y;
+                }
+                if (INJECT) {
+                    const int dd = d < 4 ? d : d + 1;
+                    if (((fbd >> (2 * j)) & 1u) && inj_burn[(rowoff + 2 * j) * 9 + dd] < pd.x) burn_inj |= 1u << (2 * j);
+                    if (((fbd >> (2 * j + 1)) & 1u) && inj_burn[(rowoff + 2 * j + 1) * 9 + dd] < pd.y)
+                        burn_inj |= 1u << (2 * j + 1);
+                }
+                c = (f2){clamp01(pd.x), clamp01(pd.y)};
             } else {
-                qn[i] = f ? __fmul_rn(qn[i], __fsub_rn(1.0f, clamp01(pd))) : qn[i];
+                c = pk_mul_clamp01(t, ps);
+            }
+            if (!INJECT) {
+                const f2 x = (f2){1.0f, 1.0f} - c;
+                const uint32_t x0 = bfi32(sbit(fbd, 2 * j), __float_as_uint(x.x), 0x3F800000u);
+                const uint32_t x1 = bfi32(sbit(fbd, 2 * j + 1), __float_as_uint(x.y), 0x3F800000u);
+                qn2[j] = qn2[j] * (f2){__uint_as_float(x0), __uint_as_float(x1)};
             }
         }
-        __builtin_amdgcn_sched_barrier(0);  // one direction's 64 B per lane in flight at a time
+#pragma unroll
+        for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(qn2[j]));  // finish this direction's products here
+        if (d + 2 < 8) load_ps(d + 2, psc);  // refill the buffer just consumed
+        if (d == 6) load_ages();              // its buffer is free from here on
+        __builtin_amdgcn_sched_barrier(0);    // two directions' 64 B per lane in flight
     }
 
-    uint32_t agew[8];
-    if (vec) {
-        const uint4 a0 = *reinterpret_cast<const uint4*>(aEi + lo);
-        const uint4 a1 = *reinterpret_cast<const uint4*>(aEi + lo + 8);
-        agew[0] = a0.x; agew[1] = a0.y; agew[2] = a0.z; agew[3] = a0.w;
-        agew[4] = a1.x; agew[5] = a1.y; agew[6] = a1.z; agew[7] = a1.w;
-    } else {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) agew[k] = 0u;
+    // ---- draws: burn / grow masks and the packed new-fire ages NA (two cells per word)
+    uint32_t burn, grow, NA[8];
+    if (INJECT) {
+        burn = burn_inj;
+        grow = 0u;
 #pragma unroll
         for (int i = 0; i < 16; ++i)
-            if (row_ok && cbase + i < W) agew[i >> 1] |= (uint32_t)(uint16_t)aEi[lo + i] << (16 * (i & 1));
+            if (((okB & emptyB) >> i) & 1u) grow |= (uint32_t)(inj_grow[rowoff + i] < p.p_tree) << i;
+#pragma unroll
+        for (int pp = 0; pp < 8; ++pp) {
+            const uint32_t n0 = ((burn >> (2 * pp)) & 1u) ? (uint32_t)inj_age[rowoff + 2 * pp] : 0u;
+            const uint32_t n1 = ((burn >> (2 * pp + 1)) & 1u) ? (uint32_t)inj_age[rowoff + 2 * pp + 1] : 0u;
+            NA[pp] = __builtin_amdgcn_perm(n1, n0, 0x05040100u);
+        }
+    } else {
+        // Philox block for cell index pair lin>>1; word pair (2h, 2h+1) for h = lin & 1.
+        // burn iff u < 1 - qn  <=>  (main >> 8) < (1 - qn) * 2^24 (exact power-of-two scaling);
+        // grow iff u < p_tree. Cells that need no draw cannot change through them (qn = 1 -> 1-qn = 0).
+        const uint32_t needB = okB & ((treeB & anyfire) | (p.p_tree > 0.0f ? emptyB : 0u));
+        const float pt24 = __fmul_rn(p.p_tree, 16777216.0f);
+        const bool odd = !FAST && (lin0 & 1u);  // FAST: W even -> every lane's first cell is even
+        uint32_t Dt = 0u, Dg = 0u;
+#pragma unroll
+        for (int pp = 0; pp < 8; ++pp) {
+            const uint32_t nd = (needB >> (2 * pp)) & 3u;
+            const uint32_t cA = (lin0 + (uint32_t)(2 * pp)) >> 1;
+            u32x4 XA = u32x4{0u, 0u, 0u, 0u}, XB = u32x4{0u, 0u, 0u, 0u};
+            uint32_t m0, m1, a0, a1;
+            if (!odd) {
+                if (nd) XA = philox4x32_10(u32x4{cA, env_id, step, GCA_TAG_ALEX_CELL}, k0, k1);
+                m0 = XA.x; a0 = XA.y; m1 = XA.z; a1 = XA.w;
+            } else {
+                if (nd & 1u) XA = philox4x32_10(u32x4{cA, env_id, step, GCA_TAG_ALEX_CELL}, k0, k1);
+                if (nd & 2u) XB = philox4x32_10(u32x4{cA + 1u, env_id, step, GCA_TAG_ALEX_CELL}, k0, k1);
+                m0 = XA.z; a0 = XA.w; m1 = XB.x; a1 = XB.y;
+            }
+            const f2 thr = ((f2){1.0f, 1.0f} - qn2[pp]) * (f2){16777216.0f, 16777216.0f};
+            const float u0 = (float)(m0 >> 8), u1 = (float)(m1 >> 8);
+            Dt = push_lt(Dt, u0, thr.x);
+            Dt = push_lt(Dt, u1, thr.y);
+            Dg = push_lt(Dg, u0, pt24);
+            Dg = push_lt(Dg, u1, pt24);
+            const uint32_t n0 = (uint32_t)randint_ms(a0, p.age_lo, p.age_hi);
+            const uint32_t n1 = (uint32_t)randint_ms(a1, p.age_lo, p.age_hi);
+            NA[pp] = __builtin_amdgcn_perm(n1, n0, 0x05040100u);
+            __builtin_amdgcn_sched_barrier(0);  // one Philox block in flight per lane
+        }
+        burn = (__builtin_bitreverse32(Dt) >> 16) & treeB & okB;
+        grow = (__builtin_bitreverse32(Dg) >> 16) & emptyB & okB;
     }
 
-    // ---- draws and the rule, two cells (one Philox block) at a time
-    uint32_t outw[4] = {0u, 0u, 0u, 0u}, nagew[8];
-    int cntT = 0, cntF = 0, cntE = 0;
+    // ---- the rule on masks: TREE -> FIRE (burn), EMPTY -> TREE (grow), FIRE -> EMPTY (age <= 1)
+    uint32_t le1acc = 0u;  // age <= 1  <=>  sat(age - 2) < 0 (saturating i16: exact for every int16)
 #pragma unroll
     for (int pp = 0; pp < 8; ++pp) {
-        bool burn[2] = {false, false}, grow[2] = {false, false}, need[2];
-        int new_age[2] = {p.age_lo, p.age_lo};
+        const i16x2 y = __builtin_elementwise_sub_sat(bitcast_<i16x2>(agew[pp]), (i16x2){2, 2});
+        le1acc |= (bitcast_<uint32_t>(y) >> (15 - 2 * pp)) & ((1u << (2 * pp)) | (1u << (16 + 2 * pp)));
+    }
+    const uint32_t le1 = (le1acc & 0x5555u) | ((le1acc >> 15) & 0xAAAAu);
+    const uint32_t newF = burn | (fireB & ~le1);
+    const uint32_t newT = (treeB & ~burn) | grow;
+    const uint32_t newE = (emptyB & ~grow) | (fireB & le1);
+    const uint32_t keepB = ~(treeB | emptyB | fireB) & 0xFFFFu;  // codes outside {empty, tree, fire}: unchanged
+    // output bytes: one v_perm_b32 per word, selector 0/1/2 -> empty/tree/fire code, 4+m -> own byte m
+    const uint32_t codes = (p.empty & 0xFFu) | ((p.tree & 0xFFu) << 8) | ((p.fire & 0xFFu) << 16);
+    uint32_t sel[4];
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int i = 2 * pp + h;
-            const bool ok = (okbits >> i) & 1u, is_tree = (treebits >> i) & 1u, is_empty = (emptybits >> i) & 1u;
-            const bool nb = (anyfire >> i) & 1u;
-            if (INJECT) {
-                need[h] = false;
-                burn[h] = (burnbits >> i) & 1u;
-                if (burn[h]) new_age[h] = inj_age[rowoff + i];
-                if (ok && is_empty) grow[h] = inj_grow[rowoff + i] < p.p_tree;
-            } else {
-                need[h] = ok && ((is_tree && nb) || (is_empty && p.p_tree > 0.0f));
-            }
-        }
-        if (!INJECT) {
-            // Philox block for cell index pair lin>>1; word pair (2h, 2h+1) for h = lin & 1
-            const uint32_t linA = lin0 + (uint32_t)(2 * pp);
-            const uint32_t cA = linA >> 1, cB = (linA + 1u) >> 1;
-            u32x4 XA = u32x4{0u, 0u, 0u, 0u}, XB;
-            if (need[0] || (need[1] && cA == cB))
-                XA = philox4x32_10(u32x4{cA, env_id, step, GCA_TAG_ALEX_CELL}, k0, k1);
-            XB = XA;
-            if (need[1] && cA != cB) XB = philox4x32_10(u32x4{cB, env_id, step, GCA_TAG_ALEX_CELL}, k0, k1);
-            const bool hA = linA & 1u, hB = (linA + 1u) & 1u;
-            const uint32_t mains[2] = {hA ? XA.z : XA.x, hB ? XB.z : XB.x};
-            const uint32_t auxs[2] = {hA ? XA.w : XA.y, hB ? XB.w : XB.y};
+    for (int j = 0; j < 4; ++j) sel[j] = spread4(newT >> (4 * j)) + 2u * spread4(newF >> (4 * j));
+    if (keepB) {
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int i = 2 * pp + h;
-                if (need[h]) {
-                    if ((treebits >> i) & 1u) {
-                        burn[h] = u01_f32(mains[h]) < __fsub_rn(1.0f, qn[i]);
-                        new_age[h] = randint_ms(auxs[h], p.age_lo, p.age_hi);
-                    } else {
-                        grow[h] = u01_f32(mains[h]) < p.p_tree;
-                    }
-                }
-            }
-        }
+        for (int j = 0; j < 4; ++j) sel[j] |= (spread4(keepB >> (4 * j)) * 0xFFu) & 0x07060504u;
+    }
+    uint32_t outw[4], nagew[8];
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int i = 2 * pp + h;
-            const int x = (int)((own[i >> 2] >> (8 * (i & 3))) & 0xFFu);
-            const int age = (int)(int16_t)(agew[i >> 1] >> (16 * (i & 1)));
-            const bool is_tree = x == p.tree, is_empty = x == p.empty, is_fire = x == p.fire;
-            int nx = x;
-            if (is_tree && burn[h]) nx = p.fire;
-            else if (is_empty && grow[h]) nx = p.tree;
-            else if (is_fire && age <= 1) nx = p.empty;
-            int na = (nx == p.fire && !is_fire) ? new_age[h] : age;
-            if (is_fire) na -= 1;
-            if (h) nagew[pp] |= (uint32_t)(uint16_t)na << 16;
-            else nagew[pp] = (uint32_t)(uint16_t)na;
-            outw[i >> 2] |= (uint32_t)(nx & 0xFF) << (8 * (i & 3));
-            if ((okbits >> i) & 1u) {
-                cntT += nx == p.tree;
-                cntF += nx == p.fire;
-                cntE += nx == p.empty;
-            }
-        }
+    for (int j = 0; j < 4; ++j) outw[j] = __builtin_amdgcn_perm(own[j], codes, sel[j]);
+    // ages: FIRE cells age - 1 (also when they burn out), new fires the drawn age, others unchanged
+    const uint32_t CF = (fireB & 0x5555u) | (((fireB >> 1) & 0x5555u) << 16);
+    const uint32_t CB = (burn & 0x5555u) | (((burn >> 1) & 0x5555u) << 16);
+#pragma unroll
+    for (int pp = 0; pp < 8; ++pp) {
+        const u16x2 fh = bitcast_<u16x2>((CF >> (2 * pp)) & 0x00010001u);
+        const uint32_t a1 = bitcast_<uint32_t>(bitcast_<u16x2>(agew[pp]) - fh);
+        const uint32_t bm = ((CB >> (2 * pp)) & 0x00010001u) * 0xFFFFu;
+        nagew[pp] = bfi32(bm, NA[pp], a1);
     }
 
     // ---------------- stores
@@ -412,6 +549,8 @@ __global__ __launch_bounds__(256, 4) void alex_step_kernel(
         }
     }
     if (counts) {
+        int cntT = __builtin_popcount(newT & okB), cntF = __builtin_popcount(newF & okB),
+            cntE = __builtin_popcount(newE & okB);
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) {
             cntT += __shfl_xor(cntT, off);
@@ -449,9 +588,17 @@ void launch_alex(const gca_alex_params& p, int E, int H, int W, const uint8_t* g
     const int tiles_r = (H + TH - 1) / TH, tiles_c = (W + TW - 1) / TW;
     constexpr int RS = R < 2 ? 2 : R;
     constexpr int RR = TH + 2 * RS;
-    const size_t lds = sizeof(uint32_t) * (RR + 1) * CWP + sizeof(uint16_t) * RR * (CW / 16);
-    hipLaunchKernelGGL((alex_step_kernel<R, MODE>), dim3((unsigned)((int64_t)E * tiles_r * tiles_c)), dim3(256), lds, st,
-                       p, H, W, tiles_r, tiles_c, gi, go, ai, ao, veg, den, dous, ps, wi, rs, ib, ig, ia, po, counts);
+    const size_t lds = sizeof(uint32_t) * (RR + 1) * CWP + sizeof(uint16_t) * RR * (CW / 16) + sizeof(float) * 16;
+    const dim3 grid((unsigned)((int64_t)E * tiles_r * tiles_c));
+    const bool fast = MODE == 0 && W % TW == 0 && H % TH == 0 &&
+                      ((((uintptr_t)gi) | ((uintptr_t)go) | ((uintptr_t)ai) | ((uintptr_t)ao) | ((uintptr_t)veg) |
+                        ((uintptr_t)den) | ((uintptr_t)dous) | ((uintptr_t)ps)) & 15u) == 0;
+    if (fast)  // production shape: no per-lane bounds checks (instantiated for the Philox mode only)
+        hipLaunchKernelGGL((alex_step_kernel<R, MODE, MODE == 0>), grid, dim3(256), lds, st, p, H, W, tiles_r, tiles_c,
+                           gi, go, ai, ao, veg, den, dous, ps, wi, rs, ib, ig, ia, po, counts);
+    else
+        hipLaunchKernelGGL((alex_step_kernel<R, MODE, false>), grid, dim3(256), lds, st, p, H, W, tiles_r, tiles_c,
+                           gi, go, ai, ao, veg, den, dous, ps, wi, rs, ib, ig, ia, po, counts);
 }
 
 template <int MODE>
