@@ -163,19 +163,27 @@ def bench_windy(args, world, rank, device, pg):
     from gymca_amd._lib import call
     from gymca_amd.forest_fire.bulldozer import BatchedForestFireBulldozerEnv
 
+    from gymca_amd.graph import StepGraph
+
     E, N = 1024, 256
     env = BatchedForestFireBulldozerEnv(E, N, N, device=device, seed=0x5EED, env_offset=rank * E,
                                         materialize_obs=False)
     env.reset()
     action = torch.zeros((E, 2), dtype=torch.int32, device=device)
-    st = dev.stream_ptr(device)
 
-    def env_step(events):
-        call("gca_random_actions", dev.ptr(action), E, env.env_offset, 9, dev.ptr(env.rng_step), st)
+    def one_step():
+        # actions drawn on the device from each env's own counter, then the whole env step
+        call("gca_random_actions", dev.ptr(action), E, env.env_offset, 9, dev.ptr(env.rng_step),
+             dev.stream_ptr(device))
         env.step(action)
 
     K = max(args.steps, 40)
-    dt_env, _ = timed_loop(env_step, K, args.warmup, pg, device)
+    dt_eager, _ = timed_loop(lambda ev: one_step(), K, args.warmup, pg, device)
+    # the same steps replayed from one HIP graph per G env steps (no host launch overhead)
+    G = 8
+    graph = StepGraph(one_step, n_steps=G, device=device)
+    Kg = max(K // G, 5)
+    dt_env, _ = timed_loop(lambda ev: graph.replay(), Kg, 2, pg, device)
     # CA-only (steps[E] = 1 forced), dense variant {0:.1, 3:.6, 25:.3}
     g = env.grids()
     u = torch.rand(g.shape, device=device)
@@ -197,7 +205,9 @@ def bench_windy(args, world, rank, device, pg):
     dt_ca, kern = timed_loop(ca_step, K, args.warmup, pg, device)
     return {
         "config": "ForestFireBulldozer 256x256, 1024 envs/GPU, WindyForestFire",
-        "env_steps_per_s": world * E * K / dt_env,
+        "env_steps_per_s": world * E * Kg * G / dt_env,
+        "env_steps_per_s_eager": world * E * K / dt_eager,
+        "env_step_graph": f"hipGraph of {G} env steps (random actions + RepeatCA/Windy passes + Move/Modify + reward)",
         "ca_only_cell_updates_per_s": world * E * N * N * K / dt_ca,
         "ca_kernel_ms": kern * 1e3,
         "ca_achieved_gbs": WINDY_BYTES_PER_CELL * E * N * N / kern / 1e9,
@@ -233,6 +243,43 @@ def cpu_baseline(args):
             "sample": f"{Es} envs x {N}x{N}, {steps} Alexandridis steps, oracle/gca_oracle.c (gcc -O2, 1 thread)"}
 
 
+def measured_traffic(args):
+    """HBM bytes per alex_step launch from the committed rocprofv3 PMC summary
+    (profiles/pmc_traffic.json, written by scripts/pmc_summary.py: 2*FETCH_SIZE + WRITE_SIZE,
+    gfx950 correction) — only when this run is the profiled workload."""
+    if args.envs != 4096 or args.size != 256:
+        return None
+    tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        data = json.load(open(tf))
+    except (ValueError, OSError):
+        return None
+    for k, v in data.items():  # the Philox-mode kernel at R = 6 (N = 256)
+        if k.startswith("alex_step<6, 0"):
+            return v.get("bytes_per_launch")
+    return None
+
+
+def copy_bandwidth(device, nbytes=2 << 30, reps=10):
+    """Live device-to-device copy rate (GB/s, read + write) of torch's copy kernel on this GPU, reported
+    beside the 8 TB/s spec (SURVEY.md §8d asks for both). It is a lower bound on the practical ceiling:
+    scripts/bw_probe.hip measures the alex_step access pattern itself."""
+    import torch
+
+    a = torch.empty(nbytes, dtype=torch.uint8, device=device)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e.record()
+    e.synchronize()
+    gbs = 2.0 * nbytes * reps / (s.elapsed_time(e) * 1e-3) / 1e9
+    del a, b
+    return gbs
+
+
 def main():
     args = parse()
     world, rank, device, pg = setup_dist(args)
@@ -243,13 +290,8 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args)
-    traffic = None
-    tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(tf):
-        try:
-            traffic = json.load(open(tf)).get("alex_step_bytes_per_launch")
-        except (ValueError, OSError):
-            traffic = None
+    traffic = measured_traffic(args)
+    copy_gbs = copy_bandwidth(device)
     if rank == 0:
         out = {
             "metric": "cell-updates/sec, 4096x(256x256) ForestFireBulldozer (Alexandridis CA), per-GPU batch",
@@ -273,7 +315,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": alex["achieved_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": alex["achieved_gbs"] / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "alex_step_kernel", "kernel_ms": alex["kernel_ms"],
-                         "algorithmic_bytes_per_cell": ALEX_BYTES_PER_CELL},
+                         "algorithmic_bytes_per_cell": ALEX_BYTES_PER_CELL,
+                         "device_copy_gbs": copy_gbs},
             "cpu_baseline": cpu,
             "secondary": secondary,
         }

@@ -9,6 +9,15 @@
 #include <cstdio>
 #include <cstdint>
 
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef unsigned u4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ntl(const float4* p) {
+    const f4v v = __builtin_nontemporal_load((const f4v*)p);
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void nts(float4 v, float4* p) { __builtin_nontemporal_store((f4v){v.x, v.y, v.z, v.w}, (f4v*)p); }
+__device__ __forceinline__ void nts(uint4 v, uint4* p) { __builtin_nontemporal_store((u4v){v.x, v.y, v.z, v.w}, (u4v*)p); }
+
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("{\"error\": \"%s\"}\n", hipGetErrorString(e_)); return 1; } } while (0)
 
 __global__ void copy_k(const float4* __restrict__ a, float4* __restrict__ b, size_t n) {
@@ -22,7 +31,29 @@ __global__ void read_k(const float4* __restrict__ a, float* __restrict__ out, si
     }
     if (s == 1234.5f) out[0] = s;
 }
+__global__ __launch_bounds__(256) void copy4_k(const float4* __restrict__ a, float4* __restrict__ b, size_t n) {
+    // 4 independent float4 per lane per iteration (4 KiB per wave in flight)
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i + 3 * stride < n; i += 4 * stride) {
+        const float4 v0 = a[i], v1 = a[i + stride], v2 = a[i + 2 * stride], v3 = a[i + 3 * stride];
+        b[i] = v0; b[i + stride] = v1; b[i + 2 * stride] = v2; b[i + 3 * stride] = v3;
+    }
+}
+__global__ __launch_bounds__(256) void copy4nt_k(const float4* __restrict__ a, float4* __restrict__ b, size_t n) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i + 3 * stride < n; i += 4 * stride) {
+        const float4 v0 = ntl(a + i), v1 = ntl(a + i + stride), v2 = ntl(a + i + 2 * stride), v3 = ntl(a + i + 3 * stride);
+        nts(v0, b + i); nts(v1, b + i + stride); nts(v2, b + i + 2 * stride); nts(v3, b + i + 3 * stride);
+    }
+}
+// one tile per block, contiguous (one-shot, like alex_step): 16 KiB per block
+__global__ __launch_bounds__(256) void copy_tile_k(const float4* __restrict__ a, float4* __restrict__ b) {
+    const size_t base = (size_t)blockIdx.x * 1024 + threadIdx.x * 4;
+    const float4 v0 = a[base], v1 = a[base + 1], v2 = a[base + 2], v3 = a[base + 3];
+    b[base] = v0; b[base + 1] = v1; b[base + 2] = v2; b[base + 3] = v3;
+}
 // one lane = 16 consecutive cells of one row; one block = 256 lanes = 16 rows x 256 cols (one tile)
+template <bool NTL, bool NTS>
 __global__ __launch_bounds__(256) void alex_pattern_k(const uint8_t* __restrict__ g, uint8_t* __restrict__ go,
                                                       const int16_t* __restrict__ a, int16_t* __restrict__ ao,
                                                       const uint8_t* __restrict__ v, const uint8_t* __restrict__ d,
@@ -43,15 +74,27 @@ __global__ __launch_bounds__(256) void alex_pattern_k(const uint8_t* __restrict_
     for (int dd = 0; dd < 8; ++dd) {
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
-            const float4 p4 = *(const float4*)(pE + (size_t)dd * HW + 4 * m);
+            const float4* src = (const float4*)(pE + (size_t)dd * HW + 4 * m);
+            const float4 p4 = NTL ? ntl(src) : *src;
             acc += p4.x + p4.y + p4.z + p4.w;
         }
     }
     const uint32_t mix = (acc > 1e30f) ? 1u : 0u;
-    *(uint4*)(go + off) = make_uint4(g4.x ^ v4.x ^ mix, g4.y ^ d4.y, g4.z ^ u4.z, g4.w);
-    *(uint4*)(ao + off) = make_uint4(a0.x, a0.y ^ mix, a0.z, a0.w);
-    *(uint4*)(ao + off + 8) = a1;
+    const uint4 o0 = make_uint4(g4.x ^ v4.x ^ mix, g4.y ^ d4.y, g4.z ^ u4.z, g4.w);
+    const uint4 o1 = make_uint4(a0.x, a0.y ^ mix, a0.z, a0.w);
+    if (NTS) {
+        nts(o0, (uint4*)(go + off));
+        nts(o1, (uint4*)(ao + off));
+        nts(a1, (uint4*)(ao + off + 8));
+    } else {
+        *(uint4*)(go + off) = o0;
+        *(uint4*)(ao + off) = o1;
+        *(uint4*)(ao + off + 8) = a1;
+    }
 }
+
+#define TIME10(launch, out_ms) do { launch; CK(hipEventRecord(e0)); for (int i_ = 0; i_ < 10; ++i_) { launch; } \
+    CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1)); CK(hipEventElapsedTime(&out_ms, e0, e1)); out_ms /= 10; } while (0)
 
 int main() {
     const size_t nbytes = (size_t)8 << 30;  // 8 GiB copy source
@@ -66,21 +109,20 @@ int main() {
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     float ms;
-    const int blocks = 256 * 8 * 4;
-    copy_k<<<blocks, 256>>>(A, B, n4);
-    CK(hipEventRecord(e0));
-    for (int i = 0; i < 10; ++i) copy_k<<<blocks, 256>>>(A, B, n4);
-    CK(hipEventRecord(e1));
-    CK(hipEventSynchronize(e1));
-    CK(hipEventElapsedTime(&ms, e0, e1));
-    const double copy_gbs = 2.0 * nbytes * 10 / (ms * 1e-3) / 1e9;
-    read_k<<<blocks, 256>>>(A, out, n4);
-    CK(hipEventRecord(e0));
-    for (int i = 0; i < 10; ++i) read_k<<<blocks, 256>>>(A, out, n4);
-    CK(hipEventRecord(e1));
-    CK(hipEventSynchronize(e1));
-    CK(hipEventElapsedTime(&ms, e0, e1));
-    const double read_gbs = 1.0 * nbytes * 10 / (ms * 1e-3) / 1e9;
+    printf("{");
+    const int bl[3] = {2048, 8192, 32768};
+    for (int k = 0; k < 3; ++k) {
+        TIME10((copy_k<<<bl[k], 256>>>(A, B, n4)), ms);
+        printf("\"copy_b%d_gbs\": %.1f, ", bl[k], 2.0 * nbytes / (ms * 1e-3) / 1e9);
+        TIME10((copy4_k<<<bl[k], 256>>>(A, B, n4)), ms);
+        printf("\"copy4_b%d_gbs\": %.1f, ", bl[k], 2.0 * nbytes / (ms * 1e-3) / 1e9);
+        TIME10((copy4nt_k<<<bl[k], 256>>>(A, B, n4)), ms);
+        printf("\"copy4nt_b%d_gbs\": %.1f, ", bl[k], 2.0 * nbytes / (ms * 1e-3) / 1e9);
+    }
+    TIME10((copy_tile_k<<<(unsigned)(n4 / 1024), 256>>>(A, B)), ms);
+    printf("\"copy_tile_gbs\": %.1f, ", 2.0 * nbytes / (ms * 1e-3) / 1e9);
+    TIME10((read_k<<<8192, 256>>>(A, out, n4)), ms);
+    printf("\"read_gbs\": %.1f, ", 1.0 * nbytes / (ms * 1e-3) / 1e9);
     CK(hipFree(A));
     CK(hipFree(B));
     // alex pattern: E = 4096, 256 x 256
@@ -94,15 +136,13 @@ int main() {
     CK(hipMalloc(&ps, 32 * cells));
     CK(hipMemset(ps, 0, 32 * cells));
     const int nblk = E * (HW / 4096);
-    alex_pattern_k<<<nblk, 256>>>(g, go, a, ao, v, d, du, ps, HW);
-    CK(hipEventRecord(e0));
-    for (int i = 0; i < 10; ++i) alex_pattern_k<<<nblk, 256>>>(g, go, a, ao, v, d, du, ps, HW);
-    CK(hipEventRecord(e1));
-    CK(hipEventSynchronize(e1));
-    CK(hipEventElapsedTime(&ms, e0, e1));
-    const double alex_ms = ms / 10;
-    const double alex_gbs = 41.0 * cells / (alex_ms * 1e-3) / 1e9;
-    printf("{\"copy_gbs\": %.1f, \"read_gbs\": %.1f, \"alex_pattern_ms\": %.4f, \"alex_pattern_gbs\": %.1f}\n", copy_gbs,
-           read_gbs, alex_ms, alex_gbs);
+    TIME10((alex_pattern_k<false, false><<<nblk, 256>>>(g, go, a, ao, v, d, du, ps, HW)), ms);
+    printf("\"alex_pattern_ms\": %.4f, \"alex_pattern_gbs\": %.1f, ", ms, 41.0 * cells / (ms * 1e-3) / 1e9);
+    TIME10((alex_pattern_k<true, false><<<nblk, 256>>>(g, go, a, ao, v, d, du, ps, HW)), ms);
+    printf("\"alex_pattern_ntl_ms\": %.4f, ", ms);
+    TIME10((alex_pattern_k<false, true><<<nblk, 256>>>(g, go, a, ao, v, d, du, ps, HW)), ms);
+    printf("\"alex_pattern_nts_ms\": %.4f, ", ms);
+    TIME10((alex_pattern_k<true, true><<<nblk, 256>>>(g, go, a, ao, v, d, du, ps, HW)), ms);
+    printf("\"alex_pattern_ntls_ms\": %.4f}\n", ms);
     return 0;
 }

@@ -222,3 +222,41 @@ def test_full_size_windy_properties(device):
         w9 = np.insert(wind, 4, 0.0).reshape(3, 3)
         ref = owindy.windy_step(before[e].cpu().numpy().astype(np.int64), w9, np.full((3, 3), 0.5))
         assert np.array_equal(after[e].cpu().numpy(), ref)
+
+
+def test_batched_env_graph_replay_equals_eager(device):
+    """A HIP-graph replay of G env steps (device action sampling + the whole env step) leaves
+    every env in exactly the state G eager steps leave it in (gymca_amd/graph.py)."""
+    import torch
+
+    from gymca_amd import _device as dev
+    from gymca_amd._lib import call
+    from gymca_amd.forest_fire.bulldozer import BatchedForestFireBulldozerEnv
+    from gymca_amd.graph import StepGraph
+
+    E, N, G = 64, 64, 6
+    envs = [BatchedForestFireBulldozerEnv(E, N, N, device=device, seed=3, materialize_obs=False) for _ in range(2)]
+    acts = [torch.zeros((E, 2), dtype=torch.int32, device=device) for _ in range(2)]
+    for env in envs:
+        env.reset(seed=11)
+
+    def stepper(k):
+        def f():
+            call("gca_random_actions", dev.ptr(acts[k]), E, 0, 5, dev.ptr(envs[k].rng_step), dev.stream_ptr(device))
+            envs[k].step(acts[k])
+        return f
+
+    graph = StepGraph(stepper(0), n_steps=G, device=device, warmup=2)  # warm-up = 2 eager steps
+    eager = stepper(1)
+    for _ in range(2):
+        eager()
+    for _ in range(3):
+        graph.replay()
+        for _ in range(G):
+            eager()
+    torch.cuda.synchronize(device)
+    a, b = envs
+    assert torch.equal(a.grids(), b.grids())
+    for name in ("pos", "accu", "rng_step", "done", "counts", "reward"):
+        ta, tb = getattr(a, name), getattr(b, name)
+        assert torch.equal(torch.nan_to_num(ta), torch.nan_to_num(tb)), name
