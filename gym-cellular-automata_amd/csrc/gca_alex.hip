@@ -295,7 +295,7 @@ __global__ __launch_bounds__(256, 4) void alex_step_kernel(
     f2 ph2[8], dz2[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        ph2[j] = (f2){0.0f, 0.0f};
+        ph2[j] = (f2){p.heat0, p.heat0};  // 0 (JAX rule) or the classic constant p_h
         dz2[j] = (f2){0.0f, 0.0f};
     }
     const float w_in_minus_bd = __fsub_rn(p.dous_inner, p.dous_border);
@@ -504,7 +504,17 @@ __global__ __launch_bounds__(256, 4) void alex_step_kernel(
         const i16x2 y = __builtin_elementwise_sub_sat(bitcast_<i16x2>(agew[pp]), (i16x2){2, 2});
         le1acc |= (bitcast_<uint32_t>(y) >> (15 - 2 * pp)) & ((1u << (2 * pp)) | (1u << (16 + 2 * pp)));
     }
-    const uint32_t le1 = (le1acc & 0x5555u) | ((le1acc >> 15) & 0xAAAAu);
+    uint32_t le1 = (le1acc & 0x5555u) | ((le1acc >> 15) & 0xAAAAu);
+    if (p.burnout_eq1) {  // classic rule: burn out iff age == 1 (uniform branch)
+        uint32_t eqacc = 0u;
+#pragma unroll
+        for (int pp = 0; pp < 8; ++pp) {
+            const u16x2 x = bitcast_<u16x2>(agew[pp] ^ 0x00010001u);  // half == 0 <=> age == 1
+            const uint32_t z = bitcast_<uint32_t>(x - (u16x2){1, 1}) & ~bitcast_<uint32_t>(x) & 0x80008000u;
+            eqacc |= (z >> (15 - 2 * pp)) & ((1u << (2 * pp)) | (1u << (16 + 2 * pp)));
+        }
+        le1 = (eqacc & 0x5555u) | ((eqacc >> 15) & 0xAAAAu);
+    }
     const uint32_t newF = burn | (fireB & ~le1);
     const uint32_t newT = (treeB & ~burn) | grow;
     const uint32_t newE = (emptyB & ~grow) | (fireB & le1);

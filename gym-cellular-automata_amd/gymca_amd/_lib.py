@@ -66,6 +66,8 @@ class AlexParams(ctypes.Structure):
         ("fire", c_int32),
         ("n_winds", c_int32),
         ("winds", (c_float * 9) * 16),
+        ("heat0", c_float),
+        ("burnout_eq1", c_int32),
     ]
 
 

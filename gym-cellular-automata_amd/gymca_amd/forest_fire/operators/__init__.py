@@ -1,5 +1,5 @@
 """GPU operators with the reference's names (forest_fire/operators/__init__.py:1-20)."""
-from .ca_alexandridis import PartiallyObservableForestFireJax
+from .ca_alexandridis import PartiallyObservableForestFire, PartiallyObservableForestFireJax
 from .ca_DrosselSchwabl import ForestFire
 from .ca_windy import WindyForestFire
 from .move_modify import Modify, Move, MoveModify
@@ -8,5 +8,5 @@ from .repeat_ca import RepeatCA
 # The JAX-suffixed operators of the reference are served by the same classes.
 MoveJax, ModifyJax, MoveModifyJax, RepeatCAJax = Move, Modify, MoveModify, RepeatCA
 
-__all__ = ["WindyForestFire", "PartiallyObservableForestFireJax", "ForestFire", "Move", "Modify", "MoveModify",
-           "RepeatCA", "MoveJax", "ModifyJax", "MoveModifyJax", "RepeatCAJax"]
+__all__ = ["WindyForestFire", "PartiallyObservableForestFire", "PartiallyObservableForestFireJax", "ForestFire",
+           "Move", "Modify", "MoveModify", "RepeatCA", "MoveJax", "ModifyJax", "MoveModifyJax", "RepeatCAJax"]

@@ -208,3 +208,130 @@ class PartiallyObservableForestFireJax(Operator):
         if return_probs:
             return new_grid, out_ctx, shared_context, probs.cpu().numpy().reshape(shape + (8,))
         return new_grid, out_ctx, shared_context
+
+
+# ---------------------------------------------------------------------------- classic variant
+# PartiallyObservableForestFire (reference ca_alexandridis.py:18-221, the NumPy per-cell operator):
+# p_burn = p_h (1 + p_veg[veg]) (1 + p_den[den]) wind[i,j] exp(0.078 slope[r,c,i,j]) with the constant
+# p_h = 0.58 (:92-99), no heat kernel and no dousing; TREE with a FIRE neighbour burns iff any burning
+# neighbour's draw is below p_burn (:104-111), new fire age randint[4, 11) (:111); EMPTY -> TREE w.p.
+# p_tree (:171-177); FIRE: age -= 1 and EMPTY when it reaches 0 (:179-183); then the wind change
+# (:212-220). Pinecone spotting (:184-210) is not part of this operator (the
+# reference path draws from the global numpy RNG through `jax.numpy`, which has no `random`, so it
+# cannot run) — documented in DESIGN.md.
+CLASSIC_VEG = {1: -0.3, 2: 0.0, 3: 0.3, 4: 0.6, 5: 1.0}  # :92
+CLASSIC_DEN = {1: -0.4, 2: 0.0, 3: 0.3, 4: 0.6, 5: 1.0}  # :93
+CLASSIC_P_H = 0.58  # :94
+CLASSIC_AGE = (4, 11)  # :111, :131
+
+
+def make_classic_params(empty, tree, fire, winds, p_tree, seed, env_offset=0):
+    """gca_alex_params for the classic rule: heat0 = p_h, all heat / dousing weights 0, classic tables,
+    ages [4, 11), burn-out when the decremented age reaches 0."""
+    p = AlexParams()
+    p.R = 1
+    p.heat0 = float(np.float32(CLASSIC_P_H))
+    p.burnout_eq1 = 1
+    veg = [1.0 + CLASSIC_VEG[max(1, min(5, i))] for i in range(6)]
+    den = [1.0 + CLASSIC_DEN[max(1, min(5, i))] for i in range(6)]
+    for i in range(6):
+        p.veg1p[i], p.den1p[i] = float(np.float32(veg[i])), float(np.float32(den[i]))
+    p.p_tree = float(np.float32(p_tree))
+    p.age_lo, p.age_hi = CLASSIC_AGE
+    p.seed = int(seed) & (2**64 - 1)
+    p.env_offset = int(env_offset)
+    p.empty, p.tree, p.fire = int(empty), int(tree), int(fire)
+    wm = wind_matrices(winds)
+    if not 1 <= len(wm) <= 16:
+        raise ValueError("1..16 wind matrices supported")
+    p.n_winds = len(wm)
+    for i, m in enumerate(wm):
+        for j in range(9):
+            p.winds[i][j] = float(m.reshape(9)[j])
+    return p
+
+
+class PartiallyObservableForestFire(Operator):
+    """Drop-in for the classic operator (reference ca_alexandridis.py:18-221) on the device.
+
+    `update(grid, action, context)` follows the reference contract: context holds winds (n, 2, 3, 3),
+    wind_index, density, vegetation, slope (H, W, 3, 3), altitude, p_tree, p_wind_change, fire_age;
+    fire_age and wind_index are updated IN the context dict (the reference mutates it, :146-217) and
+    `(new_grid, context)` is returned. Draws: Philox keyed by the operator's seed with a per-call step
+    counter, or `draws=` with the reference's own arrays (burn (H,W,3,3) uniforms, grow (H,W), age
+    (H,W) ints, optional wind_u / wind_k) for an exact replay of the rule.
+    """
+
+    grid_dependant = True
+    action_dependant = False
+    context_dependant = True
+
+    deterministic = False
+
+    def __init__(self, empty, tree, fire, *args, **kwargs):
+        super().__init__(*args, **kwargs)
+        self.empty, self.tree, self.fire = empty, tree, fire
+        dev.check_u8_codes((empty, tree, fire))
+        if self.context_space is None:
+            self.context_space = Box(0.0, 1.0, shape=(2,), dtype=TYPE_BOX)
+        self._step = 0
+
+    def update(self, grid, action, context, *, draws=None, return_probs=False):
+        import torch
+
+        device = dev.require_device()
+        g = np.asarray(grid)
+        H, W = g.shape
+        veg_h, den_h = np.asarray(context["vegetation"]), np.asarray(context["density"])
+        for name, arr, table in (("vegetation", veg_h, CLASSIC_VEG), ("density", den_h, CLASSIC_DEN)):
+            bad = ~np.isin(arr, list(table))
+            if np.any(bad):  # the reference's dict lookup raises KeyError (:92-93)
+                raise KeyError(f"{name} value {arr[bad].reshape(-1)[0]!r} outside 1..5")
+        age_h = np.asarray(context["fire_age"])
+        if np.any(np.abs(age_h) > 32767) or np.any(np.rint(age_h) != age_h):
+            raise ValueError("fire_age must hold integers in the int16 range")
+
+        def d(x, dtype, shp):
+            return dev.to_device(np.ascontiguousarray(np.asarray(x).reshape(shp)), dtype, device)
+
+        grid_in = d(g.astype(np.uint8), torch.uint8, (1, H, W))
+        age_in = d(age_h.astype(np.int16), torch.int16, (1, H, W))
+        veg = d(veg_h.astype(np.uint8), torch.uint8, (1, H, W))
+        den = d(den_h.astype(np.uint8), torch.uint8, (1, H, W))
+        dous = torch.zeros((1, H, W), dtype=torch.uint8, device=device)
+        slope = d(np.asarray(context["slope"], dtype=np.float32), torch.float32, (1, H, W, 9))
+        p_slope = torch.empty((1, 8, H, W), dtype=torch.float32, device=device)
+        widx = d(np.asarray(context["wind_index"]).reshape(1).astype(np.int32), torch.int32, (1,))
+        rng_step = torch.full((1,), self._step, dtype=torch.int32, device=device)
+        p = make_classic_params(self.empty, self.tree, self.fire, context["winds"], context.get("p_tree", 0.0),
+                                self.philox_seed)
+        st = dev.stream_ptr(device)
+        call("gca_alex_prepare_slope", dev.ptr(slope), dev.ptr(p_slope), 1, H, W, st)
+        grid_out, age_out = torch.empty_like(grid_in), torch.empty_like(age_in)
+        inj = [None, None, None]
+        wu = wk = None
+        if draws is not None:
+            inj = [d(np.asarray(draws["burn"], np.float32), torch.float32, (1, H, W, 9)),
+                   d(np.asarray(draws["grow"], np.float32), torch.float32, (1, H, W)),
+                   d(np.asarray(draws["age"], np.int32), torch.int32, (1, H, W))]
+            if "wind_u" in draws:
+                wu = d(np.asarray(draws["wind_u"], np.float32).reshape(1), torch.float32, (1,))
+                wk = d(np.asarray(draws["wind_k"], np.int32).reshape(1), torch.int32, (1,))
+        probs = torch.empty((1, H, W, 8), dtype=torch.float32, device=device) if return_probs else None
+        call("gca_alex_step", p, 1, H, W, dev.ptr(grid_in), dev.ptr(grid_out), dev.ptr(age_in), dev.ptr(age_out),
+             dev.ptr(veg), dev.ptr(den), dev.ptr(dous), dev.ptr(p_slope), dev.ptr(widx), dev.ptr(rng_step),
+             dev.ptr(inj[0]), dev.ptr(inj[1]), dev.ptr(inj[2]), dev.ptr(probs), None, st)
+        call("gca_alex_wind_change", float(np.float32(context.get("p_wind_change", 0.0))), p.n_winds, p.seed, 0,
+             dev.ptr(rng_step), dev.ptr(wu), dev.ptr(wk), dev.ptr(widx), 1, st)
+        self._step += 1
+        new_grid = grid_out.cpu().numpy().reshape(H, W).astype(g.dtype)
+        new_age = age_out.cpu().numpy().reshape(H, W)
+        if isinstance(context["fire_age"], np.ndarray) and context["fire_age"].shape == (H, W):
+            np.copyto(context["fire_age"], new_age.astype(context["fire_age"].dtype))  # in place, like :181
+        else:
+            context["fire_age"] = new_age
+        context["wind_index"] = type(context["wind_index"])(int(widx.cpu().item())) \
+            if np.isscalar(context["wind_index"]) else np.int64(widx.cpu().item())
+        if return_probs:
+            return new_grid, context, probs.cpu().numpy().reshape(H, W, 8)
+        return new_grid, context

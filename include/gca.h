@@ -127,6 +127,12 @@ typedef struct {
     int32_t empty, tree, fire; /* 0, 1, 2 in AdvancedForestFireBulldozerEnv                  */
     int32_t n_winds;
     float winds[16][9];        /* shared_context["winds"][i][0] wind matrices (row-major 3x3)  */
+    float heat0;               /* initial value of the heat sum: 0 for the JAX rule; the classic
+                                  PartiallyObservableForestFire's constant p_h = 0.58 with every
+                                  heat_dw / dousing weight 0 (ca_alexandridis.py:94)             */
+    int32_t burnout_eq1;       /* 0: FIRE -> EMPTY iff age <= 1 (ca_alexandridis_jax.py:389);
+                                  1: iff age == 1, i.e. the decremented age hits 0 (classic
+                                  ca_alexandridis.py:181-183). Ages are decremented either way. */
 } gca_alex_params;
 
 /* p_slope[e][d][r][c] = exp_f32(0.078f * slope[e][r][c][d']) for the 8 non-centre d'

@@ -15,7 +15,8 @@ class OracleAlexParams(ctypes.Structure):
                 ("p_tree", ctypes.c_float), ("age_lo", ctypes.c_int32), ("age_hi", ctypes.c_int32),
                 ("seed", ctypes.c_uint64), ("env_offset", ctypes.c_int32), ("empty", ctypes.c_int32),
                 ("tree", ctypes.c_int32), ("fire", ctypes.c_int32), ("n_winds", ctypes.c_int32),
-                ("winds", (ctypes.c_float * 9) * 16)]
+                ("winds", (ctypes.c_float * 9) * 16), ("heat0", ctypes.c_float),
+                ("burnout_eq1", ctypes.c_int32)]
 
 
 _lib = None

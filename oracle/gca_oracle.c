@@ -16,7 +16,9 @@
  *   injected: TREE -> FIRE iff exists fire neighbour d with u[d] < p_d (:379-383)
  *   philox  : TREE -> FIRE iff u(main) < 1 - prod_{fire d} (1 - clamp01(p_d)), where the cell with
  *             index lin uses words (2h, 2h+1), h = lin & 1, of Philox(lin >> 1, env, step, ALXC)
- *   EMPTY -> TREE iff u < p_tree; FIRE -> EMPTY iff age <= 1; ages (:394-423).
+ *   EMPTY -> TREE iff u < p_tree; FIRE -> EMPTY iff age <= 1 (age == 1 with burnout_eq1, the
+ *   classic ca_alexandridis.py:181-183); ages (:394-423). heat starts at heat0 (0, or the classic
+ *   constant p_h = 0.58 of ca_alexandridis.py:94 with zero heat / dousing weights).
  */
 #include <math.h>
 #include <stdlib.h>
@@ -38,6 +40,8 @@ typedef struct {
     int32_t empty, tree, fire;
     int32_t n_winds;
     float winds[16][9];
+    float heat0;
+    int32_t burnout_eq1;
 } oracle_alex_params;
 
 /* ------------------------------------------------------------------ Philox4x32-10 */
@@ -125,7 +129,7 @@ static void alex_env(const oracle_alex_params* p, int e, int H, int W, const uin
         for (int c = 0; c < W; ++c) {
             const long cell = (long)r * W + c;
             /* box sums from the summed-area tables (clamped to the grid = zero padding) */
-            float ph = 0.0f, dz = 0.0f;
+            float ph = p->heat0, dz = 0.0f;
             const int KS = R < 2 ? 2 : R;
             for (int k = 0; k <= KS; ++k) {
                 const int r0 = r - k < 0 ? 0 : r - k, r1 = r + k + 1 > H ? H : r + k + 1;
@@ -185,7 +189,7 @@ static void alex_env(const oracle_alex_params* p, int e, int H, int W, const uin
             int nx = x;
             if (is_tree && burn) nx = p->fire;
             else if (is_empty && grow) nx = p->tree;
-            else if (is_fire && age[cell] <= 1) nx = p->empty;
+            else if (is_fire && (p->burnout_eq1 ? age[cell] == 1 : age[cell] <= 1)) nx = p->empty;
             int na = (nx == p->fire && !is_fire) ? new_age : age[cell];
             if (is_fire) na -= 1;
             go[cell] = (uint8_t)nx;

@@ -118,3 +118,44 @@ def test_burn_law_matches_independent_directions():
     law = 1 - (1 - np.clip(pd[0], 0, 1)) * (1 - np.clip(pd[6], 0, 1))
     freq = burned[8, 8] / (E * steps)
     assert abs(freq - law) < 4 * np.sqrt(law * (1 - law) / (E * steps)) + 1e-3
+
+
+# ------------------------------------------------------------------ classic variant (row a8)
+def _classic_inputs(ctx):
+    H, W = ctx["grid"].shape
+    age = ctx["fire_age"].astype(np.int16)[None]
+    slope = np.asarray(ctx["slope"], np.float32).reshape(1, H, W, 9)
+    return (ctx["grid"][None], age, ctx["vegetation"].astype(np.uint8)[None], ctx["density"].astype(np.uint8)[None],
+            np.zeros((1, H, W), np.uint8), alex_c.prepare_slope(slope), np.array([ctx["wind_index"]], np.int32))
+
+
+@pytest.mark.parametrize("H,W,seed", [(12, 12, 0), (17, 23, 1), (32, 32, 2)])
+def test_c_oracle_classic_matches_classic_restatement(H, W, seed):
+    """The kernel's evaluation order with the classic parameters (heat0 = p_h, classic tables,
+    ages [4, 11), burn-out at age 0) against the per-cell float64 restatement of
+    ca_alexandridis.py:71-183 with the same injected draws."""
+    from gymca_amd.forest_fire.operators.ca_alexandridis import make_classic_params
+    from oracle import alexandridis_classic as cl
+
+    rng = np.random.default_rng(seed)
+    ctx = cl.random_context(rng, H, W)
+    dr = cl.random_draws(rng, H, W)
+    ng, na, _, rp = cl.update(ctx["grid"], ctx, dr, 0, 1, 2)
+    p = make_classic_params(0, 1, 2, ctx["winds"], ctx["p_tree"], 5)
+    grid, age, veg, den, dous, ps, widx = _classic_inputs(ctx)
+    go, ao, counts, probs = alex_c.alex_step(p, grid, age, veg, den, dous, ps, widx,
+                                             inj=(dr["burn"].reshape(1, H, W, 9), dr["grow"][None], dr["age"][None]),
+                                             want_probs=True)
+    rp8 = rp.reshape(H, W, 9)[..., [0, 1, 2, 3, 5, 6, 7, 8]]
+    burning_nb = np.any(rp8 != 0, axis=-1)  # where the restatement evaluated p_burn
+    rel = np.abs(probs[0] - rp8) / np.maximum(np.abs(rp8), 1.0)
+    assert np.max(rel[burning_nb]) < 1e-6  # f32 kernel vs f64 reference arithmetic
+    diff = go[0] != ng
+    if diff.any():  # only where a uniform lies within rounding of p
+        close = np.abs(dr["burn"].reshape(H, W, 9)[..., [0, 1, 2, 3, 5, 6, 7, 8]] - rp8).min(axis=-1) < 1e-6
+        assert np.all(close[diff])
+    assert np.array_equal(ao[0][~diff], na.astype(np.int16)[~diff])
+    # classic burn-out: a FIRE with age 0 or -1 keeps burning (age -> -1 / -2), age 1 burns out
+    fire = ctx["grid"] == 2
+    assert np.all(go[0][fire & (ctx["fire_age"] <= 0)] == 2)
+    assert np.all(go[0][fire & (ctx["fire_age"] == 1)] == 0)

@@ -248,3 +248,71 @@ def test_full_size_config3_step_properties(device):
                                          env.wind_index[e:e + 1].cpu().numpy(), rng_step=np.zeros(1, np.uint32))
         assert np.array_equal(g1[e].cpu().numpy(), eg[0]) and np.array_equal(a1[e].cpu().numpy(), ea[0])
         assert np.array_equal(counts[e], ec[0])
+
+
+# ------------------------------------------------------------------ classic variant (row a8)
+@pytest.mark.parametrize("H,W,seed", [(16, 16, 0), (21, 37, 1), (64, 64, 2)])
+def test_classic_dropin_matches_classic_restatement(device, H, W, seed):
+    """PartiallyObservableForestFire (ca_alexandridis.py:18-221) on the device with the reference's
+    draws injected vs the float64 per-cell restatement: grid, fire_age (mutated in the context, like
+    the reference) and wind_index."""
+    from gymca_amd.forest_fire.operators import PartiallyObservableForestFire
+    from oracle import alexandridis_classic as cl
+
+    rng = np.random.default_rng(100 + seed)
+    ctx = cl.random_context(rng, H, W)
+    dr = cl.random_draws(rng, H, W)
+    ng, na, nw, rp = cl.update(ctx["grid"], ctx, dr, 0, 1, 2)
+    op = PartiallyObservableForestFire(0, 1, 2)
+    age_obj = ctx["fire_age"]
+    new_grid, out_ctx, probs = op(ctx["grid"], None, ctx, draws=dr, return_probs=True)
+    assert out_ctx is ctx and ctx["fire_age"] is age_obj  # context mutated in place
+    rp8 = rp.reshape(H, W, 9)[..., [0, 1, 2, 3, 5, 6, 7, 8]]
+    burning_nb = np.any(rp8 != 0, axis=-1)
+    assert np.max((np.abs(probs - rp8) / np.maximum(np.abs(rp8), 1.0))[burning_nb]) < 1e-6
+    diff = new_grid != ng
+    if diff.any():
+        close = np.abs(dr["burn"].reshape(H, W, 9)[..., [0, 1, 2, 3, 5, 6, 7, 8]] - rp8).min(axis=-1) < 1e-6
+        assert np.all(close[diff])
+    assert np.array_equal(ctx["fire_age"][~diff], na[~diff])
+    assert int(ctx["wind_index"]) == nw
+
+
+@pytest.mark.parametrize("H,W", [(64, 64), (256, 256), (45, 77)])
+def test_classic_philox_bit_exact_vs_c_oracle(device, H, W):
+    """Philox mode with the classic parameters: device == C oracle, several steps."""
+    import torch
+
+    from gymca_amd import _device as dev
+    from gymca_amd._lib import call
+    from gymca_amd.forest_fire.operators.ca_alexandridis import make_classic_params
+    from oracle import alexandridis_classic as cl
+
+    E = 3
+    rng = np.random.default_rng(H + W)
+    ctxs = [cl.random_context(rng, H, W, p_tree=0.05) for _ in range(E)]
+    grid = np.stack([c["grid"] for c in ctxs])
+    age = np.stack([c["fire_age"] for c in ctxs]).astype(np.int16)
+    veg = np.stack([c["vegetation"] for c in ctxs]).astype(np.uint8)
+    den = np.stack([c["density"] for c in ctxs]).astype(np.uint8)
+    slope = np.stack([c["slope"] for c in ctxs]).reshape(E, H, W, 9).astype(np.float32)
+    widx = np.array([c["wind_index"] for c in ctxs], np.int32)
+    dous = np.zeros((E, H, W), np.uint8)
+    p = make_classic_params(0, 1, 2, ctxs[0]["winds"], 0.05, 77)
+    ps = alex_c.prepare_slope(slope)
+    T = lambda a, t: torch.as_tensor(np.ascontiguousarray(a)).to(device=device, dtype=t)
+    g_d, a_d = T(grid, torch.uint8), T(age, torch.int16)
+    v_d, n_d, du_d, ps_d, w_d = T(veg, torch.uint8), T(den, torch.uint8), T(dous, torch.uint8), T(ps, torch.float32), \
+        T(widx, torch.int32)
+    st = dev.stream_ptr(device)
+    for step in range(4):
+        rs = np.full(E, step, np.uint32)
+        go, ao, co, _ = alex_c.alex_step(p, grid, age, veg, den, dous, ps, widx, rng_step=rs)
+        g2, a2 = torch.empty_like(g_d), torch.empty_like(a_d)
+        counts = torch.empty((E, 3), dtype=torch.int32, device=device)
+        call("gca_alex_step", p, E, H, W, dev.ptr(g_d), dev.ptr(g2), dev.ptr(a_d), dev.ptr(a2), dev.ptr(v_d),
+             dev.ptr(n_d), dev.ptr(du_d), dev.ptr(ps_d), dev.ptr(w_d), dev.ptr(T(rs.view(np.int32), torch.int32)),
+             None, None, None, None, dev.ptr(counts), st)
+        assert np.array_equal(g2.cpu().numpy(), go) and np.array_equal(a2.cpu().numpy(), ao), f"step {step}"
+        assert np.array_equal(counts.cpu().numpy(), co)
+        grid, age, g_d, a_d = go, ao, g2, a2
