@@ -156,6 +156,57 @@ def bench_alex(args, world, rank, device, pg):
     return res
 
 
+def bench_config4(args, world, rank, device, pg):
+    """BASELINE config 4: AdvancedBulldozer 256x256 with the hidden foliage / altitude layers
+    (use_hidden=True), 4096 envs per GPU. The layers come from the init_utils restatement on a
+    seeded legacy stream (same draws as the reference after np.random.seed), altitude arithmetic and
+    get_slope on the device; then the same timed step as the headline with a mid-episode state."""
+    import numpy as np
+    import torch
+
+    from gymca_amd import _device as dev
+    from gymca_amd._lib import call
+    from gymca_amd.forest_fire.bulldozer import AdvancedForestFireBulldozerEnv
+
+    E, N = args.envs, args.size
+    t0 = time.perf_counter()
+    env = AdvancedForestFireBulldozerEnv(N, N, key=2, num_envs=E, use_hidden=True, device=device,
+                                         env_offset=rank * E, hidden_rng=np.random.RandomState(2 + rank))
+    torch.cuda.synchronize(device)
+    init_s = time.perf_counter() - t0
+    env.reset()
+    synthetic_state(env, rank, device)
+    action = torch.zeros((E, 2), dtype=torch.int32, device=device)
+    st = dev.stream_ptr(device)
+
+    def step(events):
+        call("gca_random_actions", dev.ptr(action), E, env.env_offset, 13, dev.ptr(env.rng_step), st)
+        if events is not None:
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            env.ca_step()
+            b.record()
+            events.append((a, b))
+        else:
+            env.ca_step()
+        call("gca_advenv_post", env.env_params, dev.ptr(action), dev.ptr(env.pos), dev.ptr(env.accu),
+             dev.ptr(env.wind_index), dev.ptr(env.time_step), dev.ptr(env.is_night), dev.ptr(env.dousing), N, N,
+             dev.ptr(env.counts), dev.ptr(env.rng_step), dev.ptr(env.reward), dev.ptr(env.done), E, st)
+
+    dt, kern = timed_loop(step, args.steps, args.warmup, pg, device)
+    out = {"config": "AdvancedBulldozer 256x256, hidden foliage/altitude layers (use_hidden=True), 4096 envs/GPU",
+           "cell_updates_per_s": world * E * N * N * args.steps / dt,
+           "env_steps_per_s": world * E * args.steps / dt,
+           "kernel_ms": kern * 1e3,
+           "achieved_gbs": ALEX_BYTES_PER_CELL * E * N * N / kern / 1e9,
+           "init_s": init_s,
+           "init": "patches + altitude draws on the host (legacy np.random order), altitude arithmetic + "
+                   "get_slope + exp on the device"}
+    del env
+    torch.cuda.empty_cache()
+    return out
+
+
 def bench_windy(args, world, rank, device, pg):
     import torch
 
@@ -215,8 +266,79 @@ def bench_windy(args, world, rank, device, pg):
     }
 
 
-def cpu_baseline(args):
-    """The oracle's C restatement (single core) on a bounded sample of the same workload."""
+def bench_windy512(args, world, rank, device, pg):
+    """BASELINE config 5: ForestFireBulldozer 512x512, 1024 envs per GPU (8192 over 8 GPUs), with the
+    RCCL all-gather of the per-env done mask + reward (9 B/env) over xGMI — per env step (eager) and
+    per 8-step rollout segment (HIP-graph replay of the 8 steps, then one gather)."""
+    import torch
+
+    from gymca_amd import _device as dev
+    from gymca_amd._lib import call
+    from gymca_amd.forest_fire.bulldozer import BatchedForestFireBulldozerEnv
+    from gymca_amd.graph import StepGraph
+
+    E, N = 1024, 512
+    env = BatchedForestFireBulldozerEnv(E, N, N, device=device, seed=0x5EED5, env_offset=rank * E,
+                                        materialize_obs=False)
+    env.reset()
+    action = torch.zeros((E, 2), dtype=torch.int32, device=device)
+    gathered = [torch.empty(E * 9, dtype=torch.uint8, device=device) for _ in range(world)] if world > 1 else None
+
+    def one_step():
+        call("gca_random_actions", dev.ptr(action), E, env.env_offset, 11, dev.ptr(env.rng_step),
+             dev.stream_ptr(device))
+        env.step(action)
+
+    def gather():
+        if gathered is not None:
+            pg.all_gather(gathered, torch.cat([env.done, env.reward.view(torch.uint8)]))
+
+    K = max(args.steps, 40)
+
+    def eager(ev):
+        one_step()
+        gather()
+
+    dt_eager, _ = timed_loop(eager, K, args.warmup, pg, device)
+    G = 8
+    graph = StepGraph(one_step, n_steps=G, device=device)
+
+    def seg(ev):
+        graph.replay()
+        gather()
+
+    Kg = max(K // G, 5)
+    dt_g, _ = timed_loop(seg, Kg, 2, pg, device)
+    return {"config": "ForestFireBulldozer 512x512, 1024 envs/GPU (BASELINE config 5 at 8 GPUs), WindyForestFire",
+            "env_steps_per_s": world * E * Kg * G / dt_g,
+            "env_steps_per_s_eager_gather_every_step": world * E * K / dt_eager,
+            "gather": "RCCL all_gather of done u8 + reward f64 per env" if world > 1 else "none (1 GPU)"}
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _cpu_threads():
+    """Host cores this process may use, capped at 16 (the GPU box's per-job CPU share)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
+def _alex_cpu_rate(args, threads, seconds):
+    """cell-updates/s of the oracle's C restatement, `threads` workers x 8 envs each (ctypes releases
+    the GIL during the call, so the threads run in parallel; no process is forked)."""
+    import threading
+
     import numpy as np
 
     from gymca_amd.forest_fire.bulldozer.init_utils import get_winds
@@ -224,23 +346,69 @@ def cpu_baseline(args):
     from oracle import alex_c
 
     N, Es = args.size, 8
-    rng = np.random.default_rng(1)
-    grid = rng.choice(np.array([0, 1, 2], np.uint8), size=(Es, N, N), p=[0.1, 0.8, 0.1])
-    age = np.where(grid == 2, rng.integers(1, 673, (Es, N, N)), 0).astype(np.int16)
-    three = np.full((Es, N, N), 3, np.uint8)
-    dous = np.zeros((Es, N, N), np.uint8)
-    ps = np.ones((Es, 8, N, N), np.float32)
-    widx = rng.integers(0, 8, Es).astype(np.int32)
     p, _ = make_alex_params(N, 0, 1, 2, np.asarray(get_winds(False), np.float32), 0.0, 1)
-    alex_c.alex_step(p, grid, age, three, three, dous, ps, widx)  # warm
+    alex_c.lib()
+    done = [0] * threads
+
+    def worker(t):
+        rng = np.random.default_rng(1 + t)
+        grid = rng.choice(np.array([0, 1, 2], np.uint8), size=(Es, N, N), p=[0.1, 0.8, 0.1])
+        age = np.where(grid == 2, rng.integers(1, 673, (Es, N, N)), 0).astype(np.int16)
+        three = np.full((Es, N, N), 3, np.uint8)
+        dous = np.zeros((Es, N, N), np.uint8)
+        ps = np.ones((Es, 8, N, N), np.float32)
+        widx = rng.integers(0, 8, Es).astype(np.int32)
+        barrier.wait()
+        t0, steps = time.perf_counter(), 0
+        while time.perf_counter() - t0 < seconds:
+            grid, age, _, _ = alex_c.alex_step(p, grid, age, three, three, dous, ps, widx,
+                                               rng_step=np.full(Es, steps, np.uint32))
+            steps += 1
+        done[t] = steps
+
+    barrier = threading.Barrier(threads + 1)
+    pool = [threading.Thread(target=worker, args=(t,)) for t in range(threads)]
+    for th in pool:
+        th.start()
+    barrier.wait()
+    t0 = time.perf_counter()
+    for th in pool:
+        th.join()
+    dt = time.perf_counter() - t0
+    return Es * N * N * sum(done) / dt, sum(done)
+
+
+def cpu_baseline(args):
+    """The oracle's C restatement of the Alexandridis step on the GPU host's cores, bounded sample:
+    (i) one core, (ii) every core this job may use (BASELINE.md CPU-baseline plan)."""
+    threads = _cpu_threads()
+    single, s1 = _alex_cpu_rate(args, 1, args.cpu_seconds / 2)
+    multi, sm = _alex_cpu_rate(args, threads, args.cpu_seconds / 2)
+    return {"value": multi, "unit": "cell-updates/s", "cores": threads, "kind": "port",
+            "sample": f"{threads} threads x 8 envs x {args.size}x{args.size}, {sm} env-batches of Alexandridis steps "
+                      f"in {args.cpu_seconds / 2:.0f} s; oracle/gca_oracle.c (gcc -O2), the reference's JAX path "
+                      f"cannot run here", "single_core_value": single, "cpu_model": _cpu_model()}
+
+
+def windy_cpu_baseline(seconds=3.0):
+    """The reference algorithm for WindyForestFire (scipy convolve2d + the three threshold masks,
+    oracle/windy.py) on one core, 256x256, with the bulldozer env's full-grid cell count per step."""
+    import numpy as np
+
+    from gymca_amd.forest_fire.bulldozer.bulldozer import DEFAULT_WIND, parse_wind
+    from oracle import windy as owindy
+
+    rng = np.random.default_rng(5)
+    grid = rng.choice(np.array([0, 3, 25]), size=(256, 256), p=[0.1, 0.6, 0.3])
+    wind = parse_wind(DEFAULT_WIND)
     steps, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < args.cpu_seconds:
-        grid, age, _, _ = alex_c.alex_step(p, grid, age, three, three, dous, ps, widx,
-                                           rng_step=np.full(Es, steps, np.uint32))
+    while time.perf_counter() - t0 < seconds:
+        grid = owindy.windy_step(grid, wind, rng.random((3, 3)))
+        np.unique(grid, return_counts=True)
         steps += 1
     dt = time.perf_counter() - t0
-    return {"value": Es * N * N * steps / dt, "unit": "cell-updates/s", "cores": 1, "kind": "port",
-            "sample": f"{Es} envs x {N}x{N}, {steps} Alexandridis steps, oracle/gca_oracle.c (gcc -O2, 1 thread)"}
+    return {"value": 256 * 256 * steps / dt, "unit": "cell-updates/s", "cores": 1, "kind": "port",
+            "sample": f"1 env 256x256, {steps} steps of the scipy restatement + cell count"}
 
 
 def measured_traffic(args):
@@ -286,10 +454,18 @@ def main():
     import torch
 
     alex = bench_alex(args, world, rank, device, pg)
+    import gc
+
+    gc.collect()
+    torch.cuda.empty_cache()
+    config4 = None if args.no_secondary else bench_config4(args, world, rank, device, pg)
     secondary = None if args.no_secondary else bench_windy(args, world, rank, device, pg)
+    config5 = None if args.no_secondary else bench_windy512(args, world, rank, device, pg)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args)
+        if secondary is not None:
+            secondary["cpu_baseline"] = windy_cpu_baseline()
     traffic = measured_traffic(args)
     copy_gbs = copy_bandwidth(device)
     if rank == 0:
@@ -319,6 +495,8 @@ def main():
                          "device_copy_gbs": copy_gbs},
             "cpu_baseline": cpu,
             "secondary": secondary,
+            "config4": config4,
+            "config5": config5,
         }
         print(json.dumps(out))
     if pg is not None:

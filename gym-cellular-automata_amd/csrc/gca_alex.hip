@@ -704,6 +704,48 @@ __global__ void alex_slope_from_altitude_kernel(const double* __restrict__ alt, 
 }
 }  // namespace
 
+namespace {
+__global__ void alex_altitude_apply_kernel(double* __restrict__ alt, int H, int W, int E,
+                                           const int32_t* __restrict__ n_hills, const double* __restrict__ hills,
+                                           const int32_t* __restrict__ n_slopes, const double* __restrict__ slopes) {
+    const int64_t HW = (int64_t)H * W;
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= HW * E) return;
+    const int e = (int)(idx / HW);
+    const int64_t cell = idx - (int64_t)e * HW;
+    const int i = (int)(cell / W), j = (int)(cell - (int64_t)i * W);
+    double a = alt[idx];
+    const int nh = min(n_hills[e], GCA_MAX_HILLS);
+    for (int h = 0; h < nh; ++h) {
+        const double* hp = hills + ((int64_t)e * GCA_MAX_HILLS + h) * 4;
+        const int cr = (int)hp[0], cc = (int)hp[1], radius = (int)hp[2];
+        const int64_t dr = i - cr, dc = j - cc;
+        const double distance = sqrt((double)(dr * dr + dc * dc));
+        if (distance < (double)radius) a = __dadd_rn(a, __dmul_rn(hp[3], cos(distance / (double)radius * M_PI / 2)));
+    }
+    const int ns = min(n_slopes[e], GCA_MAX_SLOPES);
+    for (int k = 0; k < ns; ++k) {
+        const double* sp = slopes + ((int64_t)e * GCA_MAX_SLOPES + k) * 5;
+        const int sr = (int)sp[0], sc = (int)sp[1], width = (int)sp[2], height = (int)sp[3];
+        if (i >= sr && i < min(sr + height, H) && j >= sc && j < min(sc + width, W))
+            a = __dadd_rn(a, __dmul_rn(sp[4], (double)(i - sr) / (double)height));
+    }
+    alt[idx] = a / 10.0;
+}
+}  // namespace
+
+extern "C" int gca_alex_altitude_apply(double* altitude, int E, int H, int W, const int32_t* n_hills,
+                                       const double* hills, const int32_t* n_slopes, const double* slopes,
+                                       void* stream) {
+    GCA_CHECK_ARG(altitude && n_hills && hills && n_slopes && slopes && E > 0 && H > 0 && W > 0,
+                  "altitude_apply: bad arguments");
+    const int64_t n = (int64_t)E * H * W;
+    hipLaunchKernelGGL(alex_altitude_apply_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, altitude, H, W, E, n_hills, hills, n_slopes, slopes);
+    GCA_CHECK_LAUNCH("alex_altitude_apply");
+    return GCA_OK;
+}
+
 extern "C" int gca_alex_slope_from_altitude(const double* altitude, float* p_slope, float* slope_out, int E, int H,
                                             int W, void* stream) {
     GCA_CHECK_ARG(p_slope && E > 0 && H > 0 && W > 0, "slope_from_altitude: bad arguments");

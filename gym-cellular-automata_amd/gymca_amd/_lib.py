@@ -108,6 +108,7 @@ _SIGNATURES = {
                       c_int),
     "gca_alex_wind_change": ([c_float, c_int, c_uint64, c_int, P, P, P, P, c_int, P], c_int),
     "gca_alex_slope_from_altitude": ([P, P, P, c_int, c_int, c_int, P], c_int),
+    "gca_alex_altitude_apply": ([P, c_int, c_int, c_int, P, P, P, P, P], c_int),
     "gca_advenv_post": ([POINTER(AdvEnvParams), P, P, P, P, P, P, P, c_int, c_int, P, P, P, P, c_int, P], c_int),
     "gca_reset_where": ([P, c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, P, P], c_int),
     "gca_fill_categorical": ([P, c_int64, c_int, c_int, c_uint64, P, P, c_int, P], c_int),

@@ -23,13 +23,14 @@ from ... import _device as dev
 from ..._lib import AdvEnvParams, call
 from ..operators.ca_alexandridis import alex_constants, make_alex_params
 from .bulldozer import ACTION_SETS, bulldozer_timings
-from .init_utils import get_winds, init_altitude, init_density, init_vegetation
+from .init_utils import altitude_plan, device_altitude, get_winds, init_density, init_vegetation
 
 
 class AdvancedForestFireBulldozerEnv:
     def __init__(self, nrows, ncols, key=0, num_envs=8, speed_move=0.12, speed_act=0.03, speed_multiplier=1.0,
                  pos_bull=None, pos_fire=None, t_move=None, t_shoot=None, t_any=0.001, p_tree=0.90, p_empty=0.10,
-                 use_hidden=True, middle_fire=False, enable_extensions=False, device=None, env_offset=0):
+                 use_hidden=True, middle_fire=False, enable_extensions=False, device=None, env_offset=0,
+                 hidden_rng=None):
         import torch
 
         self.device = dev.require_device(device)
@@ -87,14 +88,29 @@ class AdvancedForestFireBulldozerEnv:
         self.steps_elapsed = torch.zeros(E, dtype=torch.float32, **kw)
         self.reward_accumulated = torch.zeros(E, dtype=torch.float32, **kw)
         self._initial = None
+        self._build_context_layers(hidden_rng)
 
     # ------------------------------------------------------------------ init
-    def _hidden_layers(self, rng):
-        """density / vegetation / altitude (:182-197): init_utils restatement when use_hidden."""
+    def _build_context_layers(self, rng):
+        """density / vegetation / altitude -> slope, once per env instance like the reference's
+        constructor (advanced_bulldozer.py:182-204). With use_hidden the layers come from the
+        init_utils restatement, which consumes `rng` (default: the global np.random state, as the
+        reference does) draw for draw; altitude's arithmetic and get_slope run on the device."""
         E, H, W = self.num_envs, self.nrows, self.ncols
+        st = dev.stream_ptr(self.device)
+        self.altitude = None
         if self.use_hidden:
-            return init_density(H, W, E, rng), init_vegetation(H, W, E, rng), init_altitude(H, W, E, rng)
-        return None, None, None
+            import torch
+
+            den = init_density(H, W, E, rng)
+            veg = init_vegetation(H, W, E, rng)
+            self.density.copy_(torch.as_tensor(np.clip(den, 0, 255).astype(np.uint8), device=self.device))
+            self.vegetation.copy_(torch.as_tensor(np.clip(veg, 0, 255).astype(np.uint8), device=self.device))
+            self.altitude = device_altitude(altitude_plan(H, W, E, rng), self.device)
+        else:
+            self.density.fill_(3)
+            self.vegetation.fill_(3)
+        call("gca_alex_slope_from_altitude", dev.ptr(self.altitude), dev.ptr(self.p_slope), None, E, H, W, st)
 
     def reset(self, seed=None, options=None):
         """Initial state of advanced_bulldozer.py:650-743 for every env."""
@@ -103,16 +119,6 @@ class AdvancedForestFireBulldozerEnv:
         E, H, W = self.num_envs, self.nrows, self.ncols
         st = dev.stream_ptr(self.device)
         rng = np.random.default_rng(self.key if seed is None else seed)
-        den, veg, alt = self._hidden_layers(rng)
-        if den is not None:
-            self.density.copy_(torch.as_tensor(np.clip(den, 0, 255).astype(np.uint8), device=self.device))
-            self.vegetation.copy_(torch.as_tensor(np.clip(veg, 0, 255).astype(np.uint8), device=self.device))
-            alt_d = torch.as_tensor(alt.astype(np.float64), device=self.device)
-        else:
-            self.density.fill_(3)
-            self.vegetation.fill_(3)
-            alt_d = None
-        call("gca_alex_slope_from_altitude", dev.ptr(alt_d), dev.ptr(self.p_slope), None, E, H, W, st)
         # grid iid over {EMPTY, TREE} (p_empty, p_tree), two fires with age (N + N//2) * 2 (:650-688)
         cdf = torch.tensor([self._p_empty_init, self._p_empty_init + self._p_tree_init, 1.0], dtype=torch.float32,
                            device=self.device)

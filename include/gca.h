@@ -164,6 +164,18 @@ int gca_alex_wind_change(float p_wind_change, int n_winds, uint64_t seed, int en
 int gca_alex_slope_from_altitude(const double* altitude, float* p_slope, float* slope_out, int E, int H, int W,
                                  void* stream);
 
+/* init_altitude's arithmetic (bulldozer/utils/init_utils.py:76-116) on the device. altitude [E][H][W]
+ * holds the noise field on entry (the reference's uniform(0, 5) draws) and the altitude on return:
+ * per cell, in the reference's order, += height * cos(dist / radius * pi / 2) for every hill with
+ * dist < radius, += height_diff * (row - start_row) / height inside every slope rectangle, then / 10.
+ * hills [E][GCA_MAX_HILLS][4] = (centre row, centre col, radius, height), n_hills [E] (<= 10);
+ * slopes [E][GCA_MAX_SLOPES][5] = (start row, start col, width, height, height_diff), n_slopes [E] (<= 8).
+ * Integer fields are stored as doubles. The random draws stay on the host (legacy np.random order). */
+#define GCA_MAX_HILLS 10
+#define GCA_MAX_SLOPES 8
+int gca_alex_altitude_apply(double* altitude, int E, int H, int W, const int32_t* n_hills, const double* hills,
+                            const int32_t* n_slopes, const double* slopes, void* stream);
+
 /* --------------------------------- AdvancedForestFireBulldozer env step (batched)
  * advanced_bulldozer.py:1103-1133 minus observations, + _award/_is_done :597-633.  */
 typedef struct {

@@ -18,8 +18,13 @@ Fixture inventory:
   drossel.npz      ForestFire (Drossel-Schwabl)      ca_DrosselSchwabl.py:32-66
   helicopter.npz   ForestFireHelicopterEnv 5x5       helicopter.py:20-236
   moore.npz        moore_n                           neighbors.py:6-147
+  init_utils.npz   init_vegetation / init_density / init_altitude / get_slope after
+                   np.random.seed(k) (bulldozer/utils/init_utils.py:10-200). Those functions
+                   use numpy and the global legacy np.random state only; the module's own
+                   `import jax.numpy` / `from flax import struct` lines get empty stand-in
+                   modules here (jax and flax are not installed).
 
-Usage:  python tests/golden/make_golden.py
+Usage:  python tests/golden/make_golden.py [fixture ...]   (default: all)
 """
 import importlib.util
 import os
@@ -276,13 +281,52 @@ def gen_moore(R, rng):
     return out
 
 
+def gen_init_utils(R, rng):
+    """Hidden layers of the Advanced env from the reference's own init functions, seeded globally."""
+    import contextlib
+    import io
+
+    jax = types.ModuleType("jax")
+    jax.numpy = np
+    flax = types.ModuleType("flax")
+    flax.struct = types.SimpleNamespace(dataclass=lambda c: c)
+    saved = {k: sys.modules.get(k) for k in ("jax", "jax.numpy", "flax")}
+    sys.modules.update({"jax": jax, "jax.numpy": np, "flax": flax})
+    try:
+        iu = _load("gym_cellular_automata.forest_fire.bulldozer.utils.init_utils",
+                   f"{REF}/forest_fire/bulldozer/utils/init_utils.py")
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                sys.modules.pop(k, None)
+            else:
+                sys.modules[k] = v
+    out = {}
+    for k, (H, W, E) in enumerate([(32, 32, 3), (24, 40, 2), (64, 64, 2)]):
+        np.random.seed(1000 + k)
+        out[f"veg_{k}"] = iu.init_vegetation(H, W, E)
+        out[f"den_{k}"] = iu.init_density(H, W, E)
+        out[f"alt_{k}"] = iu.init_altitude(H, W, E)
+        with contextlib.redirect_stdout(io.StringIO()):  # get_slope prints a histogram
+            out[f"slope_{k}"] = iu.get_slope(out[f"alt_{k}"], H, W, E)
+        out[f"shape_{k}"] = np.array([H, W, E])
+        out[f"next_{k}"] = np.random.randint(0, 2**31 - 1, size=4)  # stream position after the four calls
+    out["n"] = np.array(3)
+    return out
+
+
+GENERATORS = {"windy": gen_windy, "repeat_ca": gen_repeat, "move_modify": gen_move_modify, "bulldozer": gen_bulldozer,
+              "drossel": gen_drossel, "helicopter": gen_helicopter, "moore": gen_moore, "init_utils": gen_init_utils}
+
+
 def main():
     R = load_reference()
     rng = np.random.default_rng(20260101)
-    for name, fn in [("windy", gen_windy), ("repeat_ca", gen_repeat), ("move_modify", gen_move_modify),
-                     ("bulldozer", gen_bulldozer), ("drossel", gen_drossel), ("helicopter", gen_helicopter),
-                     ("moore", gen_moore)]:
-        data = fn(R, rng)
+    names = sys.argv[1:] or list(GENERATORS)
+    for name, fn in GENERATORS.items():
+        data = fn(R, rng)  # every generator runs, in order, so the shared rng stream is unchanged
+        if name not in names:
+            continue
         path = os.path.join(HERE, f"{name}.npz")
         np.savez_compressed(path, **data)
         print(f"{name}: {os.path.getsize(path)} bytes")
