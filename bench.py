@@ -7,7 +7,7 @@ Alexandridis rule, E = 4096 envs per GPU, N = 256, use_hidden=False (veg = den =
 altitude 0 -> p_slope = 1, still read from HBM every step), mid-episode synthetic state
 (grid iid {EMPTY .1, TREE .8, FIRE .1}, fire ages iid [1, 672], wind_index iid [0, 8)),
 p_tree = 0, p_wind_change = 0.06. One timed step = random actions (device Philox) +
-the CA step (gca_alex_step) + the env step (gca_advenv_post) [+ one RCCL all_gather of the
+the CA step (gca_alex_step_es: edge-slope layout, 25 B/cell) + the env step (gca_advenv_post) [+ one RCCL all_gather of the
 per-env done mask / reward when --gpus > 1]. Weak scaling: every rank owns E envs.
 
 Also reported: the WindyForestFire bulldozer env (config 2, E = 1024) as `secondary`,
@@ -28,7 +28,10 @@ for _p in (ROOT, os.path.join(ROOT, "gym-cellular-automata_amd")):
         sys.path.insert(0, _p)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-ALEX_BYTES_PER_CELL = 41  # grid r+w 2, age r+w 4, veg 1, den 1, p_slope 32, dousing 1
+# algorithmic HBM bytes per Alexandridis cell-update: grid r+w 2, age r+w 4, veg 1, den 1,
+# dousing 1, + slopes: edge layout 4 x f32 = 16 (gca_alex_step_es), 8-plane p_slope 8 x f32 = 32
+ALEX_BYTES = {"edge": 25, "planes": 41}
+ALEX_BYTES_PER_CELL = 41  # the SURVEY.md §8d figure (8-plane layout), reported alongside
 WINDY_BYTES_PER_CELL = 2  # u8 read + u8 write
 
 
@@ -43,6 +46,7 @@ def parse():
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--slope-layout", choices=["edge", "planes"], default="edge")
     return ap.parse_args()
 
 
@@ -118,7 +122,7 @@ def bench_alex(args, world, rank, device, pg):
 
     E, N = args.envs, args.size
     env = AdvancedForestFireBulldozerEnv(N, N, key=1, num_envs=E, use_hidden=False, device=device,
-                                         env_offset=rank * E)
+                                         env_offset=rank * E, slope_layout=args.slope_layout)
     env.reset()
     synthetic_state(env, rank, device)
     action = torch.zeros((E, 2), dtype=torch.int32, device=device)
@@ -150,9 +154,17 @@ def bench_alex(args, world, rank, device, pg):
         "env_steps_per_s": world * E * args.steps / dt,
         "ms_per_step": dt / args.steps * 1e3,
         "kernel_ms": kern * 1e3,
-        "achieved_gbs": ALEX_BYTES_PER_CELL * E * N * N / kern / 1e9,
+        "achieved_gbs": ALEX_BYTES[args.slope_layout] * E * N * N / kern / 1e9,
+        "survey_equiv_gbs": ALEX_BYTES_PER_CELL * E * N * N / kern / 1e9,
         "fires_left": int((env.counts[:, 2] > 0).sum().item()),
     }
+    # the same env from its reset state (two burning cells per env, advanced_bulldozer.py:650-688): a
+    # real episode's first steps, where the fire-sparsity skip leaves most waves the 7 B/cell of
+    # grid/age/dousing traffic. Reported separately; the headline above is the dense mid-episode state.
+    env.reset()
+    dt_sp, kern_sp = timed_loop(step, args.steps, args.warmup, pg, device)
+    res["episode_start"] = {"cell_updates_per_s": world * E * N * N * args.steps / dt_sp,
+                            "kernel_ms": kern_sp * 1e3, "state": "reset state (2 fires per env), fire-sparsity skip"}
     return res
 
 
@@ -171,7 +183,8 @@ def bench_config4(args, world, rank, device, pg):
     E, N = args.envs, args.size
     t0 = time.perf_counter()
     env = AdvancedForestFireBulldozerEnv(N, N, key=2, num_envs=E, use_hidden=True, device=device,
-                                         env_offset=rank * E, hidden_rng=np.random.RandomState(2 + rank))
+                                         env_offset=rank * E, hidden_rng=np.random.RandomState(2 + rank),
+                                         slope_layout=args.slope_layout)
     torch.cuda.synchronize(device)
     init_s = time.perf_counter() - t0
     env.reset()
@@ -198,7 +211,7 @@ def bench_config4(args, world, rank, device, pg):
            "cell_updates_per_s": world * E * N * N * args.steps / dt,
            "env_steps_per_s": world * E * args.steps / dt,
            "kernel_ms": kern * 1e3,
-           "achieved_gbs": ALEX_BYTES_PER_CELL * E * N * N / kern / 1e9,
+           "achieved_gbs": ALEX_BYTES[args.slope_layout] * E * N * N / kern / 1e9,
            "init_s": init_s,
            "init": "patches + altitude draws on the host (legacy np.random order), altitude arithmetic + "
                    "get_slope + exp on the device"}
@@ -422,8 +435,9 @@ def measured_traffic(args):
         data = json.load(open(tf))
     except (ValueError, OSError):
         return None
-    for k, v in data.items():  # the Philox-mode kernel at R = 6 (N = 256)
-        if k.startswith("alex_step<6, 0"):
+    want = "alex_step<6, 0, true, %s>" % ("true" if args.slope_layout == "edge" else "false")
+    for k, v in data.items():  # the Philox-mode FAST kernel at R = 6 (N = 256) of this slope layout
+        if k == want:
             return v.get("bytes_per_launch")
     return None
 
@@ -488,10 +502,14 @@ def main():
                        "parallelism": f"env-sharded x{world}" + (", RCCL all_gather done/reward per step"
                                                                   if world > 1 and args.gather == "step" else "")},
             "env_steps_per_s": alex["env_steps_per_s"],
+            "episode_start": alex["episode_start"],
             "roofline": {"bound": "hbm", "achieved": alex["achieved_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": alex["achieved_gbs"] / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "alex_step_kernel", "kernel_ms": alex["kernel_ms"],
-                         "algorithmic_bytes_per_cell": ALEX_BYTES_PER_CELL,
+                         "kernel": "alex_step_kernel" + ("<ES>" if args.slope_layout == "edge" else ""),
+                         "kernel_ms": alex["kernel_ms"],
+                         "algorithmic_bytes_per_cell": ALEX_BYTES[args.slope_layout],
+                         "slope_layout": args.slope_layout,
+                         "survey_41B_equiv_gbs": alex["survey_equiv_gbs"],
                          "device_copy_gbs": copy_gbs},
             "cpu_baseline": cpu,
             "secondary": secondary,

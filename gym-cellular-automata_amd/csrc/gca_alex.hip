@@ -62,6 +62,32 @@ __device__ __forceinline__ uint32_t spread4(uint32_t n) { return ((n & 0xFu) * 0
 __device__ __forceinline__ uint32_t bfi32(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
 // bit i of w as an all-ones / all-zeros word (v_bfe_i32)
 __device__ __forceinline__ uint32_t sbit(uint32_t w, int i) { return (uint32_t)((int32_t)(w << (31 - i)) >> 31); }
+
+// exp_f32 (gca_common.h) on a pair: the same IEEE op sequence per half (v_pk_fma_f32 / v_pk_mul_f32 round
+// each half like the scalar op), so bit-identical with exp_f32 and the C oracle. The clamp to [-80, 80] is
+// dropped: the edge-slope exponents are 0.078 * slope with |slope| < 90 degrees (atan), |x| < 7.1.
+__device__ __forceinline__ f2 exp_f32x2(f2 x) {
+    const f2 kf = __builtin_elementwise_rint(x * (f2){1.44269504088896341f, 1.44269504088896341f});
+    f2 r = __builtin_elementwise_fma(kf, (f2){-0.693145751953125f, -0.693145751953125f}, x);
+    r = __builtin_elementwise_fma(kf, (f2){-1.42860682030941723212e-6f, -1.42860682030941723212e-6f}, r);
+    f2 p = {1.98412698412698413e-4f, 1.98412698412698413e-4f};
+    p = __builtin_elementwise_fma(p, r, (f2){1.38888888888888889e-3f, 1.38888888888888889e-3f});
+    p = __builtin_elementwise_fma(p, r, (f2){8.33333333333333333e-3f, 8.33333333333333333e-3f});
+    p = __builtin_elementwise_fma(p, r, (f2){4.16666666666666667e-2f, 4.16666666666666667e-2f});
+    p = __builtin_elementwise_fma(p, r, (f2){1.66666666666666667e-1f, 1.66666666666666667e-1f});
+    p = __builtin_elementwise_fma(p, r, (f2){0.5f, 0.5f});
+    p = __builtin_elementwise_fma(p, r * r, r);
+    p = p + (f2){1.0f, 1.0f};
+    return (f2){__uint_as_float(__float_as_uint(p.x) + ((uint32_t)(int)kf.x << 23)),
+                __uint_as_float(__float_as_uint(p.y) + ((uint32_t)(int)kf.y << 23))};
+}
+// DPP moves inside a 16-lane row (= one image row of a workgroup: lanes q = 0..15)
+__device__ __forceinline__ float dpp_from_next(float old, float src) {  // lane q <- lane q+1; lane 15 keeps old
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(src), 0x101, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float dpp_from_prev(float old, float src) {  // lane q <- lane q-1; lane 0 keeps old
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(src), 0x111, 0xF, 0xF, false));
+}
 template <class T, class S> __device__ __forceinline__ T bitcast_(S s) {
     static_assert(sizeof(T) == sizeof(S), "size");
     T t;
@@ -78,8 +104,24 @@ template <class T, class S> __device__ __forceinline__ T bitcast_(S s) {
 // rounding (packed ops round each half like the scalar op; -ffp-contract=off).
 // FAST: W % TW == 0, H % TH == 0, every array 16-B aligned (checked on the host): all per-lane bounds
 // checks and byte-wise fallbacks compile away, which also lets the waitcnt pass keep loads in flight.
-template <int R, int MODE, bool FAST>
-__global__ __launch_bounds__(256, 4) void alex_step_kernel(
+//
+// ES (edge slopes): `p_slope` is the antisymmetric edge layout of gca_alex_edge_slope_from_altitude,
+// es[e][k][r][c] = f32(raw slope of (r,c) toward neighbour k), k = 0..3 <-> (-1,-1), (-1,0), (-1,+1),
+// (0,-1) — 16 B per cell instead of 32. Direction d < 4 of cell X reads es[d][X]; d >= 4 reads
+// -es[7-d][X + off_d] (get_slope's f64 difference, division, atan and degree scaling are odd, and so is
+// the f32 cast, so slope(X -> Y) == -slope(Y -> X) exactly); p_slope = exp_f32(0.078f * slope) in-kernel,
+// and cells on the grid border get slope 0 -> p_slope = 1 (get_slope leaves their slopes 0).
+// Bit-identical to the 8-plane layout built from the same altitude (tests/test_gpu_alexandridis.py).
+//
+// Fire sparsity (MODE 0): p_slope, vegetation, density, the heat field and the per-direction products
+// only matter for TREE cells with a burning neighbour. A workgroup with no FIRE within one cell of its tile
+// skips the heat phase; a wave with no such TREE cell skips the direction pass and its loads (a real
+// episode's fire front covers a few tiles of 256). Results are unchanged (the skipped values are unused).
+#ifndef GCA_ALEX_WGS
+#define GCA_ALEX_WGS 4
+#endif
+template <int R, int MODE, bool FAST, bool ES>
+__global__ __launch_bounds__(256, GCA_ALEX_WGS) void alex_step_kernel(
     gca_alex_params p, int H, int W, int tiles_r, int tiles_c, const uint8_t* __restrict__ grid_in,
     uint8_t* __restrict__ grid_out, const int16_t* __restrict__ age_in, int16_t* __restrict__ age_out,
     const uint8_t* __restrict__ veg, const uint8_t* __restrict__ den, const uint8_t* __restrict__ dousing,
@@ -136,41 +178,57 @@ __global__ __launch_bounds__(256, 4) void alex_step_kernel(
     const int nvalid = row_ok ? min(16, W - cbase) : 0;
     const uint32_t okB = FAST ? 0xFFFFu : nvalid >= 16 ? 0xFFFFu : (nvalid > 0 ? (1u << nvalid) - 1u : 0u);
 
-    // per-cell inputs, issued before the LDS phases so their latency overlaps them
+    // per-cell inputs: the own cells now; vegetation / density once the wave knows it needs them
     // (fire ages are loaded later, after the direction pass, to keep them out of its VGPR peak)
     uint32_t own[4], vgw[4], dnw[4];
     if (vec) {
         const uint4 g4 = *reinterpret_cast<const uint4*>(gEi + lo);
-        const uint4 v4 = *reinterpret_cast<const uint4*>(vE + lo);
-        const uint4 d4 = *reinterpret_cast<const uint4*>(nE + lo);
         own[0] = g4.x; own[1] = g4.y; own[2] = g4.z; own[3] = g4.w;
-        vgw[0] = v4.x; vgw[1] = v4.y; vgw[2] = v4.z; vgw[3] = v4.w;
-        dnw[0] = d4.x; dnw[1] = d4.y; dnw[2] = d4.z; dnw[3] = d4.w;
     } else {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            vgw[k] = dnw[k] = 0x01010101u;
-            own[k] = Ep;
-        }
+        for (int k = 0; k < 4; ++k) own[k] = Ep;
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
             if (row_ok && cbase + i < W) {
                 const uint32_t sh = 8 * (i & 3);
-                vgw[i >> 2] = (vgw[i >> 2] & ~(0xFFu << sh)) | ((uint32_t)vE[lo + i] << sh);
-                dnw[i >> 2] = (dnw[i >> 2] & ~(0xFFu << sh)) | ((uint32_t)nE[lo + i] << sh);
                 own[i >> 2] = (own[i >> 2] & ~(0xFFu << sh)) | ((uint32_t)gEi[lo + i] << sh);
             }
         }
     }
+    auto load_vd = [&]() {
+        if (vec) {
+            const uint4 v4 = *reinterpret_cast<const uint4*>(vE + lo);
+            const uint4 d4 = *reinterpret_cast<const uint4*>(nE + lo);
+            vgw[0] = v4.x; vgw[1] = v4.y; vgw[2] = v4.z; vgw[3] = v4.w;
+            dnw[0] = d4.x; dnw[1] = d4.y; dnw[2] = d4.z; dnw[3] = d4.w;
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) vgw[k] = dnw[k] = 0x01010101u;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                if (row_ok && cbase + i < W) {
+                    const uint32_t sh = 8 * (i & 3);
+                    vgw[i >> 2] = (vgw[i >> 2] & ~(0xFFu << sh)) | ((uint32_t)vE[lo + i] << sh);
+                    dnw[i >> 2] = (dnw[i >> 2] & ~(0xFFu << sh)) | ((uint32_t)nE[lo + i] << sh);
+                }
+            }
+        }
+    };
 
-    // ---- p_slope software pipeline (depth 2): direction 0 is issued with the staging loads,
-    //      direction 1 right after the heat phase, so their HBM latency overlaps the heat computation; direction
-    //      d+2 is issued as soon as d is consumed.
-    //      p_slope is 78% of the kernel's bytes, so keeping two directions in flight per wave is what
-    //      keeps HBM busy while the waves compute.
-    const float* psE = p_slope + (size_t)e * 8 * HW;  // wave-uniform
-    auto load_ps = [&](int d, float4 (&v)[4]) {
-        const float* src = psE + (uint32_t)(d * (uint32_t)HW) + lo;
+    // ---- p_slope software pipeline (depth 2): the first load is issued before the heat phase,
+    //      the second right after it, so their HBM latency overlaps the heat computation; load k+2 is
+    //      issued as soon as load k is consumed. p_slope is the bulk of the kernel's bytes, so keeping
+    //      two loads in flight per wave is what keeps HBM busy while the waves compute.
+    //      8-plane layout: load k = plane k, row r.  Edge layout (ES): loads L0..L6 =
+    //      (plane 0, r) (1, r) (2, r) (3, r) (2, r+1) (1, r+1) (0, r+1); direction d uses load
+    //      LOAD_OF(d) = 0 1 2 3 3 4 5 6 (d = 3 and 4 share plane 3 of row r).
+    constexpr int NPL = ES ? 4 : 8;
+    const float* psE = p_slope + (size_t)e * NPL * HW;  // wave-uniform
+    auto load_ps = [&](int k, float4 (&v)[4]) {
+        const int plane = ES ? (k < 4 ? k : 6 - k) : k;
+        // ES rows r+1 (k >= 4): row H-1 (a border row: every value killed) reads itself instead
+        const int dr = (ES && k >= 4 && r + 1 < H) ? 1 : 0;
+        const float* src = psE + (uint32_t)(plane * (uint32_t)HW) + lo + (uint32_t)(dr * W);
         if (vec) {
 #pragma unroll
             for (int m = 0; m < 4; ++m) v[m] = *reinterpret_cast<const float4*>(src + 4 * m);
@@ -236,7 +294,7 @@ __global__ __launch_bounds__(256, 4) void alex_step_kernel(
             }
         }
     }
-    load_ps(0, psbuf[0]);  // first p_slope direction rides along with the staging loads
+    int near_fire = 0;  // a FIRE cell within one row of the tile (rows r0-1 .. r0+TH) in this thread's chunks
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
         const int ch = tid + 256 * it;
@@ -255,6 +313,7 @@ __global__ __launch_bounds__(256, 4) void alex_step_kernel(
                     __builtin_amdgcn_perm(sdw[it][j], f, 0x0C000C00u | ((4u + (uint32_t)m) << 16) | (uint32_t)m);
         }
         FB[sr * NCH + cq] = (uint16_t)bits;
+        near_fire |= (bits != 0u && sr >= RS - 1 && sr <= RS + TH) ? 1 : 0;
     }
     for (int cc = tid; cc < CWP; cc += 256) CP[cc] = 0u;
     if (tid < 16) {
@@ -264,9 +323,64 @@ __global__ __launch_bounds__(256, 4) void alex_step_kernel(
         const float ad = v <= 1 ? p.den1p[1] : v == 2 ? p.den1p[2] : v == 3 ? p.den1p[3] : v == 4 ? p.den1p[4] : p.den1p[5];
         LUT[tid] = tid < 8 ? av : ad;
     }
-    __syncthreads();
+    // MODE 0: does any TREE cell of this workgroup (wg_need) / this wave (wave_need) have a burning
+    // neighbour? The other modes evaluate every probability.
+    bool wg_need = true;
+    if (MODE == 0)
+        wg_need = __syncthreads_or(near_fire) != 0;
+    else
+        __syncthreads();
+    uint32_t treeB = 0u, emptyB = 0u;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        treeB |= eq_nib(own[j], Tp) << (4 * j);
+        emptyB |= eq_nib(own[j], Ep) << (4 * j);
+    }
+    // FIRE bits of rows r-1, r, r+1: bit j of nbw[a] <-> staged column cc0 - 1 + j (j = 0..17)
+    auto fire_rows = [&](uint32_t (&nbw)[3]) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const uint16_t* fb = FB + (rr - 1 + a) * NCH + q;
+            nbw[a] = ((uint32_t)fb[0] >> 15) | ((uint32_t)fb[1] << 1) | (((uint32_t)fb[2] & 1u) << 17);
+        }
+    };
+    // burning-neighbour mask of direction d for all 16 cells: bit i <-> cell i
+    // d = (a, b) row-major without the centre; entry (a, b) = cell (r + a - 1, c + b - 1) (:332-337)
+    auto dir_bits_of = [](const uint32_t (&nbw)[3], int d) -> uint32_t {
+        const int a = d < 3 ? 0 : (d < 5 ? 1 : 2);
+        const int b = d < 3 ? d : (d == 3 ? 0 : (d == 4 ? 2 : d - 5));
+        return (nbw[a] >> b) & 0xFFFFu;
+    };
+    bool wave_need = true;
+    if (MODE == 0) {
+        uint32_t anyf = 0u;
+        if (wg_need) {
+            uint32_t nb0[3];
+            fire_rows(nb0);
+#pragma unroll
+            for (int d = 0; d < 8; ++d) anyf |= dir_bits_of(nb0, d);
+        }
+        wave_need = __ballot((treeB & anyf & okB) != 0u) != 0ull;
+    }
+    // ES: the three edge values a lane's shifted directions take from outside its row segment
+    float e4 = 0.0f, e5 = 0.0f, e7 = 0.0f;
+    if (wave_need) {
+        load_vd();
+        load_ps(0, psbuf[0]);  // first p_slope load: in flight during the prefix and heat phases
+#if GCA_ALEX_WGS < 4
+        load_ps(1, psbuf[1]);  // (3 workgroups per CU: the second one too)
+#endif
+        if (ES) {
+            const float* es = psE + lo;
+            if (q == 15 && row_ok && cbase + 16 < W) {
+                e4 = es[3 * (uint32_t)HW + 16];                              // es[3][r][cbase+16]
+                if (r + 1 < H) e7 = es[(uint32_t)W + 16];                    // es[0][r+1][cbase+16]
+            }
+            if (q == 0 && row_ok && cbase >= 1 && r + 1 < H) e5 = es[2 * (uint32_t)HW + (uint32_t)W - 1];  // es[2][r+1][cbase-1]
+        }
+    }
     // ---------------- column prefix: columns t and t + CW/2 per thread, every load before the adds
-    if (tid < CW / 2) {
+    if (wg_need && tid < CW / 2) {
         const int pa = pcol(tid), pb = pcol(tid + CW / 2);
         uint32_t va[RR], vb[RR];
 #pragma unroll
@@ -300,54 +414,54 @@ __global__ __launch_bounds__(256, 4) void alex_step_kernel(
     }
     const float w_in_minus_bd = __fsub_rn(p.dous_inner, p.dous_border);
     auto fire_f = [](uint32_t s) -> float { return R <= 7 ? (float)(s & 0xFFu) : (float)(s & 0xFFFFu); };
+    if (wave_need) {
 #pragma unroll
-    for (int k = 0; k <= RS; ++k) {
-        uint32_t V[16 + 2 * RS];
-        const uint32_t* top = CP + (rr - k) * CWP + 17 * (q + 1);  // = pcol(cc0)
-        const uint32_t* bot = CP + (rr + k + 1) * CWP + 17 * (q + 1);
+        for (int k = 0; k <= RS; ++k) {
+            uint32_t V[16 + 2 * RS];
+            const uint32_t* top = CP + (rr - k) * CWP + 17 * (q + 1);  // = pcol(cc0)
+            const uint32_t* bot = CP + (rr + k + 1) * CWP + 17 * (q + 1);
 #pragma unroll
-        for (int j = 0; j < 16 + 2 * RS; ++j) {
-            if (j < 16 + 2 * k) {
-                const int t = j - k;                        // column cc0 + t, t in [-k, 16 + k)
-                const int off = t + (t >= 16 ? 1 : 0) - (t < 0 ? 1 : 0);  // pcol(cc0 + t) - pcol(cc0)
-                V[j] = bot[off] - top[off];
+            for (int j = 0; j < 16 + 2 * RS; ++j) {
+                if (j < 16 + 2 * k) {
+                    const int t = j - k;                                      // column cc0 + t, t in [-k, 16 + k)
+                    const int off = t + (t >= 16 ? 1 : 0) - (t < 0 ? 1 : 0);  // pcol(cc0 + t) - pcol(cc0)
+                    V[j] = bot[off] - top[off];
+                }
+                if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);  // <= 16 LDS reads in flight (VGPR budget)
             }
-            if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);  // <= 16 LDS reads in flight (VGPR budget)
-        }
-        uint32_t s = 0u, sprev = 0u;
+            uint32_t s = 0u, sprev = 0u;
 #pragma unroll
-        for (int j = 0; j <= 2 * RS; ++j)
-            if (j <= 2 * k) s += V[j];
-        const float wk = k <= R ? p.heat_dw[k] : 0.0f;
+            for (int j = 0; j <= 2 * RS; ++j)
+                if (j <= 2 * k) s += V[j];
+            const float wk = k <= R ? p.heat_dw[k] : 0.0f;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            if (i > 0) s += V[i + 2 * k] - V[i - 1];
-            if (i & 1) {
-                const int j = i >> 1;
-                if (k <= R) ph2[j] = ph2[j] + (f2){wk, wk} * (f2){fire_f(sprev), fire_f(s)};
-                const f2 dsum = {(float)(sprev >> 16), (float)(s >> 16)};
-                if (k == 1) dz2[j] = (f2){w_in_minus_bd, w_in_minus_bd} * dsum;
-                if (k == 2) dz2[j] = dz2[j] + (f2){p.dous_border, p.dous_border} * dsum;
+            for (int i = 0; i < 16; ++i) {
+                if (i > 0) s += V[i + 2 * k] - V[i - 1];
+                if (i & 1) {
+                    const int j = i >> 1;
+                    if (k <= R) ph2[j] = ph2[j] + (f2){wk, wk} * (f2){fire_f(sprev), fire_f(s)};
+                    const f2 dsum = {(float)(sprev >> 16), (float)(s >> 16)};
+                    if (k == 1) dz2[j] = (f2){w_in_minus_bd, w_in_minus_bd} * dsum;
+                    if (k == 2) dz2[j] = dz2[j] + (f2){p.dous_border, p.dous_border} * dsum;
+                }
+                sprev = s;
             }
-            sprev = s;
-        }
-        // materialise this radius' partial sums now: without it hipcc keeps all (R+1)x16 window
-        // sums live and evaluates the f32 chains at the end (-> spills at R >= 4)
+            // materialise this radius' partial sums now: without it hipcc keeps all (R+1)x16 window
+            // sums live and evaluates the f32 chains at the end (-> spills at R >= 4)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(ph2[j]), "+v"(dz2[j]));
-        __builtin_amdgcn_sched_barrier(0);
+            for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(ph2[j]), "+v"(dz2[j]));
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ph2[j] = ph2[j] - dz2[j];  // p_h = heat - dousing (:198)
+#if GCA_ALEX_WGS >= 4
+        load_ps(1, psbuf[1]);
+#endif
     }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) ph2[j] = ph2[j] - dz2[j];  // p_h = heat - dousing (:198)
-    load_ps(1, psbuf[1]);
 
     // ---- FIRE bits of rows r-1, r, r+1: bit j of nbw[a] <-> staged column cc0 - 1 + j (j = 0..17)
     uint32_t nbw[3];
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        const uint16_t* fb = FB + (rr - 1 + a) * NCH + q;
-        nbw[a] = ((uint32_t)fb[0] >> 15) | ((uint32_t)fb[1] << 1) | (((uint32_t)fb[2] & 1u) << 17);
-    }
+    fire_rows(nbw);
     asm volatile("" : "+v"(nbw[0]), "+v"(nbw[1]), "+v"(nbw[2]));  // build the 3 words now (no 9 live halfwords)
 
     const int widx = wind_index[e];
@@ -360,34 +474,8 @@ __global__ __launch_bounds__(256, 4) void alex_step_kernel(
     const bool want_prob = PROB && prob_out != nullptr;
     const uint32_t lin0 = lo;  // cell index of cell 0 within the env
 
-    // ---- cell-state masks of the lane's 16 cells
-    uint32_t treeB = 0u, emptyB = 0u;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        treeB |= eq_nib(own[j], Tp) << (4 * j);
-        emptyB |= eq_nib(own[j], Ep) << (4 * j);
-    }
     const uint32_t fireB = (nbw[1] >> 1) & 0xFFFFu;
-
-    // ---- base = (p_h * (1 + p_veg)) * (1 + p_den)   (left-to-right product of :206), clip(idx, 1, 5)
-    //      (:176-178) through the LDS table
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const int i0 = 2 * j, i1 = 2 * j + 1;
-        const uint32_t v0 = min((vgw[i0 >> 2] >> (8 * (i0 & 3))) & 0xFFu, 7u);
-        const uint32_t v1 = min((vgw[i1 >> 2] >> (8 * (i1 & 3))) & 0xFFu, 7u);
-        const uint32_t d0 = min((dnw[i0 >> 2] >> (8 * (i0 & 3))) & 0xFFu, 7u);
-        const uint32_t d1 = min((dnw[i1 >> 2] >> (8 * (i1 & 3))) & 0xFFu, 7u);
-        const f2 av = {LUT[v0], LUT[v1]}, ad = {LUT[8 + d0], LUT[8 + d1]};
-        ph2[j] = (ph2[j] * av) * ad;  // ph2 now holds base
-    }
-    // burning-neighbour mask of direction d for all 16 cells: bit i <-> cell i
-    // d = (a, b) row-major without the centre; entry (a, b) = cell (r + a - 1, c + b - 1) (:332-337)
-    auto dir_bits = [&](int d) -> uint32_t {
-        const int a = d < 3 ? 0 : (d < 5 ? 1 : 2);
-        const int b = d < 3 ? d : (d == 3 ? 0 : (d == 4 ? 2 : d - 5));
-        return (nbw[a] >> b) & 0xFFFFu;
-    };
+    auto dir_bits = [&](int d) -> uint32_t { return dir_bits_of(nbw, d); };
     uint32_t anyfire = 0u;
 #pragma unroll
     for (int d = 0; d < 8; ++d) anyfire |= dir_bits(d);
@@ -400,50 +488,117 @@ __global__ __launch_bounds__(256, 4) void alex_step_kernel(
 #pragma unroll
     for (int j = 0; j < 8; ++j) qn2[j] = (f2){1.0f, 1.0f};
     uint32_t burn_inj = 0u;
-#pragma unroll
-    for (int d = 0; d < 8; ++d) {
-        float4 (&psc)[4] = psbuf[d & 1];
-        // pin base here: otherwise the 64 direction-independent products base*wind[d] are hoisted
-        // above the loop (128 live VGPRs -> spills)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(ph2[j]));
-        // qn of non-tree / out-of-range cells is never used (burn is masked by treeB & okB)
-        const uint32_t fbd = INJECT ? (dir_bits(d) & treeB & okB) : dir_bits(d);
-        const f2 wd2 = {wind[d], wind[d]};
+    if (wave_need) {
+        // ---- base = (p_h * (1 + p_veg)) * (1 + p_den)   (left-to-right product of :206), clip(idx, 1, 5)
+        //      (:176-178) through the LDS table
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const float4 v4 = psc[j >> 1];
-            const f2 ps = (j & 1) ? (f2){v4.z, v4.w} : (f2){v4.x, v4.y};
-            const f2 t = ph2[j] * wd2;
-            f2 c;
-            if (PROB) {
-                const f2 pd = t * ps;
-                if (want_prob) {
-                    if ((okB >> (2 * j)) & 1u) prob_out[(rowoff + 2 * j) * 8 + d] = pd.x;
-                    if ((okB >> (2 * j + 1)) & 1u) prob_out[(rowoff + 2 * j + 1) * 8 + d] = pd.y;
-                }
-                if (INJECT) {
-                    const int dd = d < 4 ? d : d + 1;
-                    if (((fbd >> (2 * j)) & 1u) && inj_burn[(rowoff + 2 * j) * 9 + dd] < pd.x) burn_inj |= 1u << (2 * j);
-                    if (((fbd >> (2 * j + 1)) & 1u) && inj_burn[(rowoff + 2 * j + 1) * 9 + dd] < pd.y)
-                        burn_inj |= 1u << (2 * j + 1);
-                }
-                c = (f2){clamp01(pd.x), clamp01(pd.y)};
-            } else {
-                c = pk_mul_clamp01(t, ps);
-            }
-            if (!INJECT) {
-                const f2 x = (f2){1.0f, 1.0f} - c;
-                const uint32_t x0 = bfi32(sbit(fbd, 2 * j), __float_as_uint(x.x), 0x3F800000u);
-                const uint32_t x1 = bfi32(sbit(fbd, 2 * j + 1), __float_as_uint(x.y), 0x3F800000u);
-                qn2[j] = qn2[j] * (f2){__uint_as_float(x0), __uint_as_float(x1)};
-            }
+            const int i0 = 2 * j, i1 = 2 * j + 1;
+            const uint32_t v0 = min((vgw[i0 >> 2] >> (8 * (i0 & 3))) & 0xFFu, 7u);
+            const uint32_t v1 = min((vgw[i1 >> 2] >> (8 * (i1 & 3))) & 0xFFu, 7u);
+            const uint32_t d0 = min((dnw[i0 >> 2] >> (8 * (i0 & 3))) & 0xFFu, 7u);
+            const uint32_t d1 = min((dnw[i1 >> 2] >> (8 * (i1 & 3))) & 0xFFu, 7u);
+            const f2 av = {LUT[v0], LUT[v1]}, ad = {LUT[8 + d0], LUT[8 + d1]};
+            ph2[j] = (ph2[j] * av) * ad;  // ph2 now holds base
         }
+        // ES border handling: cells in rows 0 / H-1 or columns 0 / W-1 get p_slope = 1 (exponent 0).
+        // Rows: lane-uniform, and only the waves holding row 0 or H-1 branch into the select.
+        const int wrow0 = r0 + 4 * __builtin_amdgcn_readfirstlane(tid >> 6);
+        const bool wave_rowkill = ES && (wrow0 == 0 || wrow0 + 3 >= H - 1);
+        const bool rowkill = r == 0 || r >= H - 1;
+        const bool kill_lo = cbase == 0;
+        const int hi_idx = W - 1 - cbase;  // element holding column W-1, if in [0, 16)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(qn2[j]));  // finish this direction's products here
-        if (d + 2 < 8) load_ps(d + 2, psc);  // refill the buffer just consumed
-        if (d == 6) load_ages();              // its buffer is free from here on
-        __builtin_amdgcn_sched_barrier(0);    // two directions' 64 B per lane in flight
+        for (int d = 0; d < 8; ++d) {
+            const int ld = ES ? (d < 4 ? d : d - 1) : d;  // load consumed by direction d
+            float4 (&psc)[4] = psbuf[ld & 1];
+            f2 ps2[8];
+            if (!ES) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) ps2[j] = (j & 1) ? (f2){psc[j >> 1].z, psc[j >> 1].w}
+                                                             : (f2){psc[j >> 1].x, psc[j >> 1].y};
+            } else {
+                float a[16];
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const float4 v = psc[i >> 2];
+                    a[i] = (i & 3) == 0 ? v.x : (i & 3) == 1 ? v.y : (i & 3) == 2 ? v.z : v.w;
+                }
+                // d = 4, 7: element i <- i + 1 (cell i's right / down-right neighbour);
+                // d = 5: element i <- i - 1; the row segment's outer element comes from the next /
+                // previous lane of the 16-lane row (DPP) or, at the segment's end, from e4 / e7 / e5
+                if (d == 4 || d == 7) {
+                    const float nx = dpp_from_next(d == 4 ? e4 : e7, a[0]);
+#pragma unroll
+                    for (int i = 0; i < 15; ++i) a[i] = a[i + 1];
+                    a[15] = nx;
+                } else if (d == 5) {
+                    const float pv = dpp_from_prev(e5, a[15]);
+#pragma unroll
+                    for (int i = 15; i > 0; --i) a[i] = a[i - 1];
+                    a[0] = pv;
+                }
+                if (wave_rowkill) {
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) a[i] = rowkill ? 0.0f : a[i];
+                }
+                a[0] = kill_lo ? 0.0f : a[0];
+                if (FAST) {
+                    a[15] = hi_idx == 15 ? 0.0f : a[15];
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) a[i] = hi_idx == i ? 0.0f : a[i];
+                }
+                const float sg = d < 4 ? 0.078f : -0.078f;  // d >= 4: -es of the neighbour (exact negation)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) ps2[j] = exp_f32x2((f2){sg, sg} * (f2){a[2 * j], a[2 * j + 1]});
+            }
+            // pin base here: otherwise the 64 direction-independent products base*wind[d] are hoisted
+            // above the loop (128 live VGPRs -> spills)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(ph2[j]));
+            // qn of non-tree / out-of-range cells is never used (burn is masked by treeB & okB)
+            const uint32_t fbd = INJECT ? (dir_bits(d) & treeB & okB) : dir_bits(d);
+            const f2 wd2 = {wind[d], wind[d]};
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const f2 ps = ps2[j];
+                const f2 t = ph2[j] * wd2;
+                f2 c;
+                if (PROB) {
+                    const f2 pd = t * ps;
+                    if (want_prob) {
+                        if ((okB >> (2 * j)) & 1u) prob_out[(rowoff + 2 * j) * 8 + d] = pd.x;
+                        if ((okB >> (2 * j + 1)) & 1u) prob_out[(rowoff + 2 * j + 1) * 8 + d] = pd.y;
+                    }
+                    if (INJECT) {
+                        const int dd = d < 4 ? d : d + 1;
+                        if (((fbd >> (2 * j)) & 1u) && inj_burn[(rowoff + 2 * j) * 9 + dd] < pd.x)
+                            burn_inj |= 1u << (2 * j);
+                        if (((fbd >> (2 * j + 1)) & 1u) && inj_burn[(rowoff + 2 * j + 1) * 9 + dd] < pd.y)
+                            burn_inj |= 1u << (2 * j + 1);
+                    }
+                    c = (f2){clamp01(pd.x), clamp01(pd.y)};
+                } else {
+                    c = pk_mul_clamp01(t, ps);
+                }
+                if (!INJECT) {
+                    const f2 x = (f2){1.0f, 1.0f} - c;
+                    const uint32_t x0 = bfi32(sbit(fbd, 2 * j), __float_as_uint(x.x), 0x3F800000u);
+                    const uint32_t x1 = bfi32(sbit(fbd, 2 * j + 1), __float_as_uint(x.y), 0x3F800000u);
+                    qn2[j] = qn2[j] * (f2){__uint_as_float(x0), __uint_as_float(x1)};
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(qn2[j]));  // finish this direction's products here
+            // refill the buffer just consumed with load ld + 2 (ES: not after d = 3, whose load d = 4 reuses)
+            const int last = ES ? 6 : 7;
+            if (ld + 2 <= last && !(ES && d == 3)) load_ps(ld + 2, psc);
+            if (d == 6) load_ages();            // its buffer is free from here on
+            __builtin_amdgcn_sched_barrier(0);  // two loads' 64 B per lane in flight
+        }
+    } else {
+        load_ages();
     }
 
     // ---- draws: burn / grow masks and the packed new-fire ages NA (two cells per word)
@@ -590,7 +745,7 @@ __global__ void alex_prepare_slope_kernel(const float* __restrict__ slope, float
     }
 }
 
-template <int R, int MODE>
+template <int R, int MODE, bool ES>
 void launch_alex(const gca_alex_params& p, int E, int H, int W, const uint8_t* gi, uint8_t* go, const int16_t* ai,
                  int16_t* ao, const uint8_t* veg, const uint8_t* den, const uint8_t* dous, const float* ps,
                  const int32_t* wi, const uint32_t* rs, const float* ib, const float* ig, const int32_t* ia, float* po,
@@ -604,20 +759,20 @@ void launch_alex(const gca_alex_params& p, int E, int H, int W, const uint8_t* g
                       ((((uintptr_t)gi) | ((uintptr_t)go) | ((uintptr_t)ai) | ((uintptr_t)ao) | ((uintptr_t)veg) |
                         ((uintptr_t)den) | ((uintptr_t)dous) | ((uintptr_t)ps)) & 15u) == 0;
     if (fast)  // production shape: no per-lane bounds checks (instantiated for the Philox mode only)
-        hipLaunchKernelGGL((alex_step_kernel<R, MODE, MODE == 0>), grid, dim3(256), lds, st, p, H, W, tiles_r, tiles_c,
-                           gi, go, ai, ao, veg, den, dous, ps, wi, rs, ib, ig, ia, po, counts);
+        hipLaunchKernelGGL((alex_step_kernel<R, MODE, MODE == 0, ES>), grid, dim3(256), lds, st, p, H, W, tiles_r,
+                           tiles_c, gi, go, ai, ao, veg, den, dous, ps, wi, rs, ib, ig, ia, po, counts);
     else
-        hipLaunchKernelGGL((alex_step_kernel<R, MODE, false>), grid, dim3(256), lds, st, p, H, W, tiles_r, tiles_c,
+        hipLaunchKernelGGL((alex_step_kernel<R, MODE, false, ES>), grid, dim3(256), lds, st, p, H, W, tiles_r, tiles_c,
                            gi, go, ai, ao, veg, den, dous, ps, wi, rs, ib, ig, ia, po, counts);
 }
 
-template <int MODE>
+template <int MODE, bool ES>
 void dispatch_r(int R, const gca_alex_params& p, int E, int H, int W, const uint8_t* gi, uint8_t* go, const int16_t* ai,
                 int16_t* ao, const uint8_t* veg, const uint8_t* den, const uint8_t* dous, const float* ps,
                 const int32_t* wi, const uint32_t* rs, const float* ib, const float* ig, const int32_t* ia, float* po,
                 int32_t* counts, hipStream_t st) {
 #define GCA_ALEX_CASE(RV) \
-    case RV: launch_alex<RV, MODE>(p, E, H, W, gi, go, ai, ao, veg, den, dous, ps, wi, rs, ib, ig, ia, po, counts, st); break;
+    case RV: launch_alex<RV, MODE, ES>(p, E, H, W, gi, go, ai, ao, veg, den, dous, ps, wi, rs, ib, ig, ia, po, counts, st); break;
     switch (R) {
         GCA_ALEX_CASE(1) GCA_ALEX_CASE(2) GCA_ALEX_CASE(3) GCA_ALEX_CASE(4)
         GCA_ALEX_CASE(5) GCA_ALEX_CASE(6) GCA_ALEX_CASE(7) GCA_ALEX_CASE(8)
@@ -636,7 +791,7 @@ extern "C" int gca_alex_prepare_slope(const float* slope, float* p_slope, int E,
     return GCA_OK;
 }
 
-extern "C" int gca_alex_step(const gca_alex_params* p, int E, int H, int W, const uint8_t* grid_in, uint8_t* grid_out,
+static int alex_step_impl(bool es, const gca_alex_params* p, int E, int H, int W, const uint8_t* grid_in, uint8_t* grid_out,
                              const int16_t* age_in, int16_t* age_out, const uint8_t* veg, const uint8_t* den,
                              const uint8_t* dousing, const float* p_slope, const int32_t* wind_index,
                              const uint32_t* rng_step, const float* inj_burn, const float* inj_grow,
@@ -656,16 +811,35 @@ extern "C" int gca_alex_step(const gca_alex_params* p, int E, int H, int W, cons
         return GCA_ERR_HIP;
     }
     if (inj)
-        dispatch_r<2>(p->R, *p, E, H, W, grid_in, grid_out, age_in, age_out, veg, den, dousing, p_slope, wind_index,
+        (es ? dispatch_r<2, true> : dispatch_r<2, false>)(p->R, *p, E, H, W, grid_in, grid_out, age_in, age_out, veg, den, dousing, p_slope, wind_index,
                          rng_step, inj_burn, inj_grow, inj_age, prob_out, counts, st);
     else if (prob_out)
-        dispatch_r<1>(p->R, *p, E, H, W, grid_in, grid_out, age_in, age_out, veg, den, dousing, p_slope, wind_index,
+        (es ? dispatch_r<1, true> : dispatch_r<1, false>)(p->R, *p, E, H, W, grid_in, grid_out, age_in, age_out, veg, den, dousing, p_slope, wind_index,
                       rng_step, nullptr, nullptr, nullptr, prob_out, counts, st);
     else
-        dispatch_r<0>(p->R, *p, E, H, W, grid_in, grid_out, age_in, age_out, veg, den, dousing, p_slope, wind_index,
+        (es ? dispatch_r<0, true> : dispatch_r<0, false>)(p->R, *p, E, H, W, grid_in, grid_out, age_in, age_out, veg, den, dousing, p_slope, wind_index,
                       rng_step, nullptr, nullptr, nullptr, nullptr, counts, st);
-    GCA_CHECK_LAUNCH("alex_step");
+    GCA_CHECK_LAUNCH(es ? "alex_step_es" : "alex_step");
     return GCA_OK;
+}
+
+extern "C" int gca_alex_step(const gca_alex_params* p, int E, int H, int W, const uint8_t* grid_in, uint8_t* grid_out,
+                             const int16_t* age_in, int16_t* age_out, const uint8_t* veg, const uint8_t* den,
+                             const uint8_t* dousing, const float* p_slope, const int32_t* wind_index,
+                             const uint32_t* rng_step, const float* inj_burn, const float* inj_grow,
+                             const int32_t* inj_age, float* prob_out, int32_t* counts, void* stream) {
+    return alex_step_impl(false, p, E, H, W, grid_in, grid_out, age_in, age_out, veg, den, dousing, p_slope,
+                          wind_index, rng_step, inj_burn, inj_grow, inj_age, prob_out, counts, stream);
+}
+
+extern "C" int gca_alex_step_es(const gca_alex_params* p, int E, int H, int W, const uint8_t* grid_in,
+                                uint8_t* grid_out, const int16_t* age_in, int16_t* age_out, const uint8_t* veg,
+                                const uint8_t* den, const uint8_t* dousing, const float* edge_slope,
+                                const int32_t* wind_index, const uint32_t* rng_step, const float* inj_burn,
+                                const float* inj_grow, const int32_t* inj_age, float* prob_out, int32_t* counts,
+                                void* stream) {
+    return alex_step_impl(true, p, E, H, W, grid_in, grid_out, age_in, age_out, veg, den, dousing, edge_slope,
+                          wind_index, rng_step, inj_burn, inj_grow, inj_age, prob_out, counts, stream);
 }
 
 // ------------------------------------------------------------------ slope from altitude
@@ -703,6 +877,44 @@ __global__ void alex_slope_from_altitude_kernel(const double* __restrict__ alt, 
     }
 }
 }  // namespace
+
+// Edge layout of the same slopes (see alex_step_kernel, ES): es[e][k][r][c] = f32(raw slope of
+// (r,c) toward neighbour k), k = 0..3 <-> (-1,-1), (-1,0), (-1,+1), (0,-1), with get_slope's arithmetic
+// but WITHOUT its border zeroing (the step kernel applies that per cell); 0 where the neighbour is outside.
+namespace {
+__global__ void alex_edge_slope_from_altitude_kernel(const double* __restrict__ alt, float* __restrict__ es, int H,
+                                                     int W, int E) {
+    const int64_t HW = (int64_t)H * W;
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= HW * E) return;
+    const int e = (int)(idx / HW);
+    const int64_t cell = idx - (int64_t)e * HW;
+    const int r = (int)(cell / W), c = (int)(cell - (int64_t)r * W);
+    const double* a = alt ? alt + (int64_t)e * HW : nullptr;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int dr = k < 3 ? -1 : 0, dc = k < 3 ? k - 1 : -1;
+        const int nr = r + dr, nc = c + dc;
+        float s = 0.0f;
+        if (a && nr >= 0 && nc >= 0 && nc < W) {
+            double diff = a[cell] - a[(int64_t)nr * W + nc];
+            if (dr != 0 && dc != 0) diff /= 1.414;
+            s = (float)(atan(diff) * (180.0 / 3.14159265358979323846));
+        }
+        es[((int64_t)e * 4 + k) * HW + cell] = s;
+    }
+}
+}  // namespace
+
+extern "C" int gca_alex_edge_slope_from_altitude(const double* altitude, float* edge_slope, int E, int H, int W,
+                                                 void* stream) {
+    GCA_CHECK_ARG(edge_slope && E > 0 && H > 0 && W > 0, "edge_slope_from_altitude: bad arguments");
+    const int64_t n = (int64_t)E * H * W;
+    hipLaunchKernelGGL(alex_edge_slope_from_altitude_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, altitude, edge_slope, H, W, E);
+    GCA_CHECK_LAUNCH("alex_edge_slope_from_altitude");
+    return GCA_OK;
+}
 
 namespace {
 __global__ void alex_altitude_apply_kernel(double* __restrict__ alt, int H, int W, int E,

@@ -9,7 +9,8 @@ import os
 from ctypes import POINTER, c_double, c_float, c_int, c_int16, c_int32, c_int64, c_uint32, c_uint64, c_void_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libgca_hip.so")
+# GCA_LIB_PATH: an alternative build of the same library (A/B kernel experiments, scripts/build_variant.sh)
+LIB_PATH = os.environ.get("GCA_LIB_PATH") or os.path.join(_HERE, "_lib", "libgca_hip.so")
 
 GCA_OK = 0
 GCA_MAX_RADIUS = 8
@@ -108,6 +109,9 @@ _SIGNATURES = {
                       c_int),
     "gca_alex_wind_change": ([c_float, c_int, c_uint64, c_int, P, P, P, P, c_int, P], c_int),
     "gca_alex_slope_from_altitude": ([P, P, P, c_int, c_int, c_int, P], c_int),
+    "gca_alex_step_es": ([POINTER(AlexParams), c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
+                         c_int),
+    "gca_alex_edge_slope_from_altitude": ([P, P, c_int, c_int, c_int, P], c_int),
     "gca_alex_altitude_apply": ([P, c_int, c_int, c_int, P, P, P, P, P], c_int),
     "gca_advenv_post": ([POINTER(AdvEnvParams), P, P, P, P, P, P, P, c_int, c_int, P, P, P, P, c_int, P], c_int),
     "gca_reset_where": ([P, c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, P, P], c_int),

@@ -14,8 +14,11 @@ gca_reset_where. Observations (RGB / extension channels, :988-1101) are the next
 of SURVEY.md §8f and are not built here: `obs` carries the true grid.
 
 Device layout per env: grid u8 (ping-pong), fire_age i16 (ping-pong), vegetation /
-density / dousing u8, p_slope f32 [8][H][W] (= exp(0.078*slope), computed once at
-reset), plus per-env scalars. 41 B of HBM traffic per cell-update.
+density / dousing u8, the slopes in the antisymmetric edge layout f32 [4][H][W]
+(0.078 * slope toward the 4 preceding neighbours, built once from altitude; the step
+derives the other 4 directions and exp in-kernel: gca_alex_step_es), plus per-env
+scalars: 25 B of HBM traffic per cell-update. slope_layout="planes" keeps
+the general 8-plane p_slope f32 [8][H][W] = exp(0.078*slope) (41 B per cell-update).
 """
 import numpy as np
 
@@ -30,7 +33,7 @@ class AdvancedForestFireBulldozerEnv:
     def __init__(self, nrows, ncols, key=0, num_envs=8, speed_move=0.12, speed_act=0.03, speed_multiplier=1.0,
                  pos_bull=None, pos_fire=None, t_move=None, t_shoot=None, t_any=0.001, p_tree=0.90, p_empty=0.10,
                  use_hidden=True, middle_fire=False, enable_extensions=False, device=None, env_offset=0,
-                 hidden_rng=None):
+                 hidden_rng=None, slope_layout="edge"):
         import torch
 
         self.device = dev.require_device(device)
@@ -75,7 +78,11 @@ class AdvancedForestFireBulldozerEnv:
         self.vegetation = torch.full((E, H, W), 3, dtype=torch.uint8, **kw)
         self.density = torch.full((E, H, W), 3, dtype=torch.uint8, **kw)
         self.dousing = torch.zeros((E, H, W), dtype=torch.uint8, **kw)
-        self.p_slope = torch.ones((E, 8, H, W), dtype=torch.float32, **kw)
+        if slope_layout not in ("edge", "planes"):
+            raise ValueError("slope_layout must be 'edge' or 'planes'")
+        self.slope_layout = slope_layout
+        # edge: (E, 4, H, W) exponents for gca_alex_step_es; planes: (E, 8, H, W) p_slope for gca_alex_step
+        self.slope_data = torch.zeros((E, 4 if slope_layout == "edge" else 8, H, W), dtype=torch.float32, **kw)
         self.wind_index = torch.zeros(E, dtype=torch.int32, **kw)
         self.pos = torch.zeros((E, 2), dtype=torch.int32, **kw)
         self.accu = torch.zeros(E, dtype=torch.float32, **kw)
@@ -110,7 +117,28 @@ class AdvancedForestFireBulldozerEnv:
         else:
             self.density.fill_(3)
             self.vegetation.fill_(3)
-        call("gca_alex_slope_from_altitude", dev.ptr(self.altitude), dev.ptr(self.p_slope), None, E, H, W, st)
+        self._slopes_from(self.altitude)
+
+    def _slopes_from(self, altitude):
+        E, H, W = self.num_envs, self.nrows, self.ncols
+        st = dev.stream_ptr(self.device)
+        if self.slope_layout == "edge":
+            call("gca_alex_edge_slope_from_altitude", dev.ptr(altitude), dev.ptr(self.slope_data), E, H, W, st)
+        else:
+            call("gca_alex_slope_from_altitude", dev.ptr(altitude), dev.ptr(self.slope_data), None, E, H, W, st)
+
+    def p_slope_planes(self):
+        """The general 8-plane p_slope (E, 8, H, W) = exp_f32(0.078 * slope) of this env's altitude
+        (gca_alex_slope_from_altitude), e.g. for the oracle; the step itself may use the edge layout."""
+        import torch
+
+        if self.slope_layout == "planes":
+            return self.slope_data
+        E, H, W = self.num_envs, self.nrows, self.ncols
+        out = torch.empty((E, 8, H, W), dtype=torch.float32, device=self.device)
+        call("gca_alex_slope_from_altitude", dev.ptr(self.altitude), dev.ptr(out), None, E, H, W,
+             dev.stream_ptr(self.device))
+        return out
 
     def reset(self, seed=None, options=None):
         """Initial state of advanced_bulldozer.py:650-743 for every env."""
@@ -184,7 +212,8 @@ class AdvancedForestFireBulldozerEnv:
         if altitude is not None:
             alt = altitude if dev.is_device_tensor(altitude) else torch.as_tensor(np.asarray(altitude, np.float64),
                                                                                  device=self.device)
-            call("gca_alex_slope_from_altitude", dev.ptr(alt.contiguous()), dev.ptr(self.p_slope), None, E, H, W, st)
+            self.altitude = alt.to(self.device, torch.float64).contiguous()
+            self._slopes_from(self.altitude)
         call("gca_count_cells", dev.ptr(self.grid[self.cur]), E, H, W, self._empty, self._tree, self._fire,
              dev.ptr(self.counts), st)
 
@@ -205,9 +234,10 @@ class AdvancedForestFireBulldozerEnv:
         """The CA step alone (RepeatCAJax's one step) for every env; swaps the ping-pong buffers."""
         E, H, W = self.num_envs, self.nrows, self.ncols
         a, b = self.cur, 1 - self.cur
-        call("gca_alex_step", self.alex_params, E, H, W, dev.ptr(self.grid[a]), dev.ptr(self.grid[b]),
+        fn = "gca_alex_step_es" if self.slope_layout == "edge" else "gca_alex_step"
+        call(fn, self.alex_params, E, H, W, dev.ptr(self.grid[a]), dev.ptr(self.grid[b]),
              dev.ptr(self.age[a]), dev.ptr(self.age[b]), dev.ptr(self.vegetation), dev.ptr(self.density),
-             dev.ptr(self.dousing), dev.ptr(self.p_slope), dev.ptr(self.wind_index), dev.ptr(self.rng_step),
+             dev.ptr(self.dousing), dev.ptr(self.slope_data), dev.ptr(self.wind_index), dev.ptr(self.rng_step),
              None, None, None, None, dev.ptr(self.counts), dev.stream_ptr(self.device))
         self.cur = b
 

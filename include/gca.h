@@ -152,6 +152,23 @@ int gca_alex_step(const gca_alex_params* p, int E, int H, int W, const uint8_t* 
                   const float* inj_burn, const float* inj_grow, const int32_t* inj_age, float* prob_out,
                   int32_t* counts, void* stream);
 
+/* gca_alex_step with the slopes in the antisymmetric edge layout of gca_alex_edge_slope_from_altitude
+ * (16 B per cell instead of p_slope's 32): edge_slope (E,4,H,W) f32. Valid for slopes that come from an
+ * altitude field through get_slope (init_utils.py:166-200), the only slopes the Advanced env has
+ * (advanced_bulldozer.py:182-204); results are bit-identical to gca_alex_step on the p_slope that
+ * gca_alex_slope_from_altitude builds from the same altitude. Same replaced code and draws as above. */
+int gca_alex_step_es(const gca_alex_params* p, int E, int H, int W, const uint8_t* grid_in, uint8_t* grid_out,
+                     const int16_t* age_in, int16_t* age_out, const uint8_t* veg, const uint8_t* den,
+                     const uint8_t* dousing, const float* edge_slope, const int32_t* wind_index,
+                     const uint32_t* rng_step, const float* inj_burn, const float* inj_grow, const int32_t* inj_age,
+                     float* prob_out, int32_t* counts, void* stream);
+
+/* Edge-slope layout for gca_alex_step_es from altitude [E][H][W] f64 (NULL = flat): edge_slope[e][k][r][c] =
+ * f32(degrees(atan((alt[r][c] - alt[n]) / (1.414 if diagonal)))) toward neighbour n = k-th of
+ * (-1,-1), (-1,0), (-1,+1), (0,-1) (0 where n is outside the grid), i.e. get_slope (init_utils.py:166-200)
+ * without its border zeroing, which the step applies per cell.                                        */
+int gca_alex_edge_slope_from_altitude(const double* altitude, float* edge_slope, int E, int H, int W, void* stream);
+
 /* Wind change of PartiallyObservableForestFireJax.update (ca_alexandridis_jax.py:442-451) for E envs:
  * u < p_wind_change -> wind_index = (wind_index + k) % n_winds, k in [1, 8).
  * inj_u/inj_k injected draws, or both NULL -> Philox((0, env_offset+e, rng_step[e], ALXW)) words 0/1. */

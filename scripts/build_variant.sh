@@ -1,0 +1,18 @@
+#!/bin/bash
+# Build an A/B variant of libgca_hip.so with extra compiler flags (e.g. -DGCA_ALEX_WGS=3) into
+# gym-cellular-automata_amd/gymca_amd/_lib/variants/<name>.so; select it with GCA_LIB_PATH=<that path>.
+# Usage: bash scripts/build_variant.sh <name> <flags...>
+set -e
+NAME=$1; shift
+R=$(cd "$(dirname "$0")/.." && pwd)
+C=$R/gym-cellular-automata_amd/csrc
+O=$R/gym-cellular-automata_amd/gymca_amd/_lib/variants
+B=$C/build/variant_$NAME
+mkdir -p $O $B
+F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -Wno-unused-function -munsafe-fp-atomics $*"
+for s in gca_util gca_windy gca_env gca_alex gca_ds; do
+  /opt/rocm/bin/hipcc $F -c $C/$s.hip -o $B/$s.o &
+done
+wait
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 $B/*.o -o $O/$NAME.so
+echo $O/$NAME.so

@@ -93,6 +93,48 @@ __global__ __launch_bounds__(256) void alex_pattern_k(const uint8_t* __restrict_
     }
 }
 
+
+// edge-slope pattern (25 B/cell: the 8-plane pattern with 4 slope planes, + planes 0..2 of row r+1, which
+// the next row's lanes read as their own). COAL = 0: lane = 16 consecutive cells, 64 B contiguous per
+// lane per plane (4 x dwordx4 at stride 64 B across lanes); COAL = 1: the plane's 1 KiB row segment is
+// read as 4 instructions of 16 consecutive lanes x 16 B (lane-interleaved storage order).
+template <int COAL>
+__global__ __launch_bounds__(256) void alex_es_pattern_k(const uint8_t* __restrict__ g, uint8_t* __restrict__ go,
+                                                         const int16_t* __restrict__ a, int16_t* __restrict__ ao,
+                                                         const uint8_t* __restrict__ v, const uint8_t* __restrict__ d,
+                                                         const uint8_t* __restrict__ du, const float* __restrict__ es,
+                                                         int HW, int W) {
+    const int tiles = HW / 4096;
+    const int e = blockIdx.x / tiles, t = blockIdx.x % tiles;
+    const size_t off = (size_t)e * HW + (size_t)t * 4096 + threadIdx.x * 16;
+    const uint4 g4 = *(const uint4*)(g + off);
+    const uint4 v4 = *(const uint4*)(v + off);
+    const uint4 d4 = *(const uint4*)(d + off);
+    const uint4 u4 = *(const uint4*)(du + off);
+    const uint4 a0 = *(const uint4*)(a + off);
+    const uint4 a1 = *(const uint4*)(a + off + 8);
+    float acc = 0.f;
+    const int row = (t * 16 + (threadIdx.x >> 4));
+    const int q = threadIdx.x & 15;
+    const float* pE = es + (size_t)e * 4 * HW + (size_t)row * W;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+        const int plane = k < 4 ? k : 6 - k;
+        const int rr = (k >= 4 && row + 1 < HW / W) ? 1 : 0;
+        const float* base = pE + (size_t)plane * HW + (size_t)rr * W;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const float4* src = (const float4*)(base + (COAL ? (64 * m + 4 * q) : (16 * q + 4 * m)));
+            const float4 p4 = *src;
+            acc += p4.x + p4.y + p4.z + p4.w;
+        }
+    }
+    const uint32_t mix = (acc > 1e30f) ? 1u : 0u;
+    *(uint4*)(go + off) = make_uint4(g4.x ^ v4.x ^ mix, g4.y ^ d4.y, g4.z ^ u4.z, g4.w);
+    *(uint4*)(ao + off) = make_uint4(a0.x, a0.y ^ mix, a0.z, a0.w);
+    *(uint4*)(ao + off + 8) = a1;
+}
+
 #define TIME10(launch, out_ms) do { launch; CK(hipEventRecord(e0)); for (int i_ = 0; i_ < 10; ++i_) { launch; } \
     CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1)); CK(hipEventElapsedTime(&out_ms, e0, e1)); out_ms /= 10; } while (0)
 
@@ -143,6 +185,10 @@ int main() {
     TIME10((alex_pattern_k<false, true><<<nblk, 256>>>(g, go, a, ao, v, d, du, ps, HW)), ms);
     printf("\"alex_pattern_nts_ms\": %.4f, ", ms);
     TIME10((alex_pattern_k<true, true><<<nblk, 256>>>(g, go, a, ao, v, d, du, ps, HW)), ms);
-    printf("\"alex_pattern_ntls_ms\": %.4f}\n", ms);
+    printf("\"alex_pattern_ntls_ms\": %.4f, ", ms);
+    TIME10((alex_es_pattern_k<0><<<nblk, 256>>>(g, go, a, ao, v, d, du, ps, HW, 256)), ms);
+    printf("\"es_pattern_lane64_ms\": %.4f, \"es_pattern_lane64_gbs\": %.1f, ", ms, 25.0 * cells / (ms * 1e-3) / 1e9);
+    TIME10((alex_es_pattern_k<1><<<nblk, 256>>>(g, go, a, ao, v, d, du, ps, HW, 256)), ms);
+    printf("\"es_pattern_coal_ms\": %.4f, \"es_pattern_coal_gbs\": %.1f}\n", ms, 25.0 * cells / (ms * 1e-3) / 1e9);
     return 0;
 }

@@ -164,7 +164,7 @@ def test_advanced_env_matches_oracle_composition(device):
     g, a = case["grid"].copy(), case["age"].copy()
     veg, den = np.clip(case["veg"], 1, 5), np.clip(case["den"], 1, 5)
     dous = case["dous"].copy()
-    ps = env.p_slope.cpu().numpy()
+    ps = env.p_slope_planes().cpu().numpy()
     widx = case["widx"].copy()
     pos = env.pos.cpu().numpy().copy()
     accu = np.zeros(E, np.float32)
@@ -244,7 +244,7 @@ def test_full_size_config3_step_properties(device):
         p.env_offset = e
         eg, ea, ec, _ = alex_c.alex_step(p, g0[e:e + 1].cpu().numpy(), a0[e:e + 1].cpu().numpy(),
                                          np.full((1, N, N), 3, np.uint8), np.full((1, N, N), 3, np.uint8),
-                                         np.zeros((1, N, N), np.uint8), env.p_slope[e:e + 1].cpu().numpy(),
+                                         np.zeros((1, N, N), np.uint8), env.p_slope_planes()[e:e + 1].cpu().numpy(),
                                          env.wind_index[e:e + 1].cpu().numpy(), rng_step=np.zeros(1, np.uint32))
         assert np.array_equal(g1[e].cpu().numpy(), eg[0]) and np.array_equal(a1[e].cpu().numpy(), ea[0])
         assert np.array_equal(counts[e], ec[0])
