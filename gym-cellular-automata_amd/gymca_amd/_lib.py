@@ -91,6 +91,31 @@ class AdvEnvParams(ctypes.Structure):
     ]
 
 
+GCA_OBS_MAX_EXT = 4
+
+
+class ObsParams(ctypes.Structure):
+    """gca_obs_params (include/gca.h)."""
+
+    _fields_ = [
+        ("empty", c_int32),
+        ("tree", c_int32),
+        ("fire", c_int32),
+        ("n_ext", c_int32),
+        ("ext_skip_visibility", c_int32 * GCA_OBS_MAX_EXT),
+        ("ext_skip_blur", c_int32 * GCA_OBS_MAX_EXT),
+        ("enable_extensions", c_int32),
+        ("should_transform", c_int32),
+        ("day_length", c_int32),
+        ("color_day", (c_float * 3) * 4),
+        ("color_night", (c_float * 3) * 4),
+        ("tint_day", c_float * 3),
+        ("tint_night", c_float * 3),
+        ("n_choices", c_int32),
+        ("ext_lookup", (c_int32 * GCA_OBS_MAX_EXT) * 8),
+    ]
+
+
 P = c_void_p  # device pointers travel as plain addresses
 _SIGNATURES = {
     "gca_last_error": ([], ctypes.c_char_p),
@@ -112,6 +137,8 @@ _SIGNATURES = {
     "gca_alex_step_es": ([POINTER(AlexParams), c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
                          c_int),
     "gca_alex_edge_slope_from_altitude": ([P, P, c_int, c_int, c_int, P], c_int),
+    "gca_adv_observation": ([POINTER(ObsParams), c_int, c_int, c_int, c_int, P, P, P, P, P, P, c_int, P, P, P],
+                            c_int),
     "gca_alex_altitude_apply": ([P, c_int, c_int, c_int, P, P, P, P, P], c_int),
     "gca_advenv_post": ([POINTER(AdvEnvParams), P, P, P, P, P, P, P, c_int, c_int, P, P, P, P, c_int, P], c_int),
     "gca_reset_where": ([P, c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, P, P], c_int),

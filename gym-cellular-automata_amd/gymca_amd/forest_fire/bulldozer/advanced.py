@@ -10,8 +10,9 @@ Reference: advanced_bulldozer.py:63-1133 (JAX, vmap over num_envs). One env step
                       (advanced_bulldozer.py:1116-1127), reward -(f/(t+f+1e-8)) and done (:597-633)
 
 and `conditional_reset` (:422-518) re-injects the initial state of finished envs with
-gca_reset_where. Observations (RGB / extension channels, :988-1101) are the next row
-of SURVEY.md §8f and are not built here: `obs` carries the true grid.
+gca_reset_where. observation="rgb" adds the reference's observation (gca_adv_observation:
+RGB f32 (E, H, W, 3) of the extension/blur/visibility pipeline, :988-1101, and the reset
+observation :401-411); observation="grid" (default) returns the true u8 grid instead.
 
 Device layout per env: grid u8 (ping-pong), fire_age i16 (ping-pong), vegetation /
 density / dousing u8, the slopes in the antisymmetric edge layout f32 [4][H][W]
@@ -27,13 +28,14 @@ from ..._lib import AdvEnvParams, call
 from ..operators.ca_alexandridis import alex_constants, make_alex_params
 from .bulldozer import ACTION_SETS, bulldozer_timings
 from .init_utils import altitude_plan, device_altitude, get_winds, init_density, init_vegetation
+from .observation import make_obs_params
 
 
 class AdvancedForestFireBulldozerEnv:
     def __init__(self, nrows, ncols, key=0, num_envs=8, speed_move=0.12, speed_act=0.03, speed_multiplier=1.0,
                  pos_bull=None, pos_fire=None, t_move=None, t_shoot=None, t_any=0.001, p_tree=0.90, p_empty=0.10,
                  use_hidden=True, middle_fire=False, enable_extensions=False, device=None, env_offset=0,
-                 hidden_rng=None, slope_layout="edge"):
+                 hidden_rng=None, slope_layout="edge", observation="grid"):
         import torch
 
         self.device = dev.require_device(device)
@@ -95,6 +97,14 @@ class AdvancedForestFireBulldozerEnv:
         self.steps_elapsed = torch.zeros(E, dtype=torch.float32, **kw)
         self.reward_accumulated = torch.zeros(E, dtype=torch.float32, **kw)
         self._initial = None
+        if observation not in ("grid", "rgb"):
+            raise ValueError("observation must be 'grid' or 'rgb'")
+        self.observation = observation
+        self.enable_extensions = bool(enable_extensions)
+        # MDP(should_transform_grid = transform_grid and enable_extensions, ...) (advanced_bulldozer.py:293-302)
+        self.obs_params = make_obs_params(self._empty, self._tree, self._fire, self.enable_extensions,
+                                          self.enable_extensions, self._day_length)
+        self.rgb = torch.zeros((E, H, W, 3), dtype=torch.float32, **kw) if observation == "rgb" else None
         self._build_context_layers(hidden_rng)
 
     # ------------------------------------------------------------------ init
@@ -181,6 +191,9 @@ class AdvancedForestFireBulldozerEnv:
              dev.ptr(self.counts), st)
         self._initial = dict(grid=self.grid[0].clone(), age=self.age[0].clone(), pos=self.pos.clone(),
                              wind_index=self.wind_index.clone(), counts=self.counts.clone())
+        if self.rgb is not None:  # the reference's reset observation (advanced_bulldozer.py:405-409)
+            call("gca_adv_observation", self.obs_params, 1, E, H, W, dev.ptr(self.grid[0]), dev.ptr(self.dousing),
+                 dev.ptr(self.pos), dev.ptr(self.is_night), None, None, 0, dev.ptr(self.rgb), None, st)
         return self._obs(), self._info()
 
     def set_state(self, grid=None, fire_age=None, vegetation=None, density=None, wind_index=None, dousing=None,
@@ -224,7 +237,18 @@ class AdvancedForestFireBulldozerEnv:
                                    "density": self.density, "time_step": self.time_step, "is_night": self.is_night,
                                    "true_grid": self.grid[self.cur], "rng_step": self.rng_step},
                "position": self.pos, "time": self.accu}
-        return self.grid[self.cur], ctx
+        return (self.rgb if self.rgb is not None else self.grid[self.cur]), ctx
+
+    def render_observation(self, action=None, channels=None):
+        """The step observation (gca_adv_observation mode 0) of the current state into self.rgb; `action`
+        (E, >= 3) int32 device tensor carries the extension choice; `channels` (E, H, W, 5) u8 receives the
+        channel stack. Uses the post-step is_night / time_step to recover the pre-step day/night."""
+        E, H, W = self.num_envs, self.nrows, self.ncols
+        a = action if (action is not None and action.shape[-1] >= 3) else None
+        call("gca_adv_observation", self.obs_params, 0, E, H, W, dev.ptr(self.grid[self.cur]), dev.ptr(self.dousing),
+             dev.ptr(self.pos), dev.ptr(self.is_night), dev.ptr(self.time_step), dev.ptr(a),
+             0 if a is None else int(a.shape[-1]), dev.ptr(self.rgb), dev.ptr(channels), dev.stream_ptr(self.device))
+        return self.rgb
 
     def _info(self):
         return {"reward": self.reward, "terminated": self.done.bool(), "steps_elapsed": self.steps_elapsed,
@@ -246,13 +270,16 @@ class AdvancedForestFireBulldozerEnv:
         import torch
 
         E, H, W = self.num_envs, self.nrows, self.ncols
-        a = action if dev.is_device_tensor(action) else torch.as_tensor(np.asarray(action), device=self.device)
-        a = a.to(torch.int32).reshape(E, -1)[:, :2].contiguous()
+        full = action if dev.is_device_tensor(action) else torch.as_tensor(np.asarray(action), device=self.device)
+        full = full.to(torch.int32).reshape(E, -1).contiguous()
+        a = full[:, :2].contiguous()
         self.ca_step()
         call("gca_advenv_post", self.env_params, dev.ptr(a), dev.ptr(self.pos), dev.ptr(self.accu),
              dev.ptr(self.wind_index), dev.ptr(self.time_step), dev.ptr(self.is_night), dev.ptr(self.dousing), H, W,
              dev.ptr(self.counts), dev.ptr(self.rng_step), dev.ptr(self.reward), dev.ptr(self.done), E,
              dev.stream_ptr(self.device))
+        if self.rgb is not None:
+            self.render_observation(full)
         self.steps_elapsed += 1
         self.reward_accumulated += self.reward
         terminated = self.done.bool()

@@ -220,6 +220,40 @@ int gca_reset_where(const uint8_t* done, int E, int H, int W, uint8_t* grid, con
                     int32_t* pos, const int32_t* pos0, float* accu, int32_t* wind_index, const int32_t* wind_index0,
                     void* stream);
 
+/* ------------------------------------------- Advanced env observations (RGB)
+ * MDP.build_observation_on_extensions + grid_to_rgb_with_extensions + grid_to_rgb
+ * (advanced_bulldozer.py:988-1101) with apply_blur / apply_visibility / transform_grid /
+ * apply_extensions (bulldozer/utils/extension_utils.py:89-196).                       */
+#define GCA_OBS_MAX_EXT 4
+typedef struct {
+    int32_t empty, tree, fire;
+    int32_t n_ext;                              /* extension channels (reference registry: 2)       */
+    int32_t ext_skip_visibility[GCA_OBS_MAX_EXT];
+    int32_t ext_skip_blur[GCA_OBS_MAX_EXT];     /* (unblur: 0/1, see_invisible_fires: 1/0)          */
+    int32_t enable_extensions;                  /* MDP.enable_extensions                             */
+    int32_t should_transform;                   /* MDP.should_transform_grid                         */
+    int32_t day_length;                         /* > 0 with time_step: undo the step's is_night toggle */
+    float color_day[4][3];                      /* empty, tree, fire, position (0..255 as f32)       */
+    float color_night[4][3];
+    float tint_day[3], tint_night[3];           /* water tint of doused cells                        */
+    int32_t n_choices;                          /* extension-choice ids (create_up_to_k_mappings)     */
+    int32_t ext_lookup[8][GCA_OBS_MAX_EXT];     /* id -> binary extension flags                       */
+} gca_obs_params;
+
+/* rgb [E][H][W][3] f32 (and, nullable, channels [E][H][W][3 + n_ext] u8 = transformed grid, 0, 0,
+ * extension channels) for E envs.
+ * mode 0 (env step, advanced_bulldozer.py:1120): grid/position after the step, dousing and is_night
+ *   before it (pass the post-step is_night with time_step to undo its toggle); action [E][action_stride]
+ *   full actions (move, shoot, extension choice): the choice (column 2, clamped to n_choices - 1) maps
+ *   to binary extension flags through ext_lookup (_create_full_actions :308-330); action NULL or
+ *   action_stride < 3 = no extension active.
+ * mode 1 (reset, :401-411): the reference applies grid_to_rgb_with_extensions to the raw (H, W)
+ *   grid; its broadcasting gives rgb[r][c] = colour(grid[c][k]) with k = 3 + the first row holding a
+ *   positive value in columns 3.. (clamped), or k = 0 — reproduced as is (square grids only).   */
+int gca_adv_observation(const gca_obs_params* p, int mode, int E, int H, int W, const uint8_t* grid,
+                        const uint8_t* dousing, const int32_t* pos, const int32_t* is_night, const int32_t* time_step,
+                        const int32_t* action, int action_stride, float* rgb, uint8_t* channels, void* stream);
+
 /* Synthetic inputs for benches/tests (Philox, GCA_TAG_INIT / GCA_TAG_ACTION). */
 int gca_fill_categorical(uint8_t* out, int64_t n_per_env, int E, int env_offset, uint64_t seed,
                          const float* cdf, const uint8_t* values, int n_values, void* stream);

@@ -62,6 +62,9 @@ int main(void) {
   P(gca_alex_params, winds)
   printf("gca_advenv_params %zu\n", sizeof(gca_advenv_params));
   P(gca_advenv_params, day_length) P(gca_advenv_params, seed) P(gca_advenv_params, right_mask)
+  printf("gca_obs_params %zu\n", sizeof(gca_obs_params));
+  P(gca_obs_params, ext_skip_blur) P(gca_obs_params, day_length) P(gca_obs_params, color_night)
+  P(gca_obs_params, tint_night) P(gca_obs_params, ext_lookup)
   return 0;
 }
 """
@@ -77,7 +80,7 @@ def test_struct_layouts_match_the_header(tmp_path):
     out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
     got = dict(line.rsplit(" ", 1) for line in out if line)
     py = {"gca_bulldozer_params": _lib.BulldozerParams, "gca_alex_params": _lib.AlexParams,
-          "gca_advenv_params": _lib.AdvEnvParams}
+          "gca_advenv_params": _lib.AdvEnvParams, "gca_obs_params": _lib.ObsParams}
     for key, val in got.items():
         if "." in key:
             t, f = key.split(".")
