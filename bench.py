@@ -122,7 +122,8 @@ def bench_alex(args, world, rank, device, pg):
 
     E, N = args.envs, args.size
     env = AdvancedForestFireBulldozerEnv(N, N, key=1, num_envs=E, use_hidden=False, device=device,
-                                         env_offset=rank * E, slope_layout=args.slope_layout)
+                                         env_offset=rank * E, slope_layout=args.slope_layout, observation="rgb",
+                                         enable_extensions=True)
     env.reset()
     synthetic_state(env, rank, device)
     action = torch.zeros((E, 2), dtype=torch.int32, device=device)
@@ -158,6 +159,28 @@ def bench_alex(args, world, rank, device, pg):
         "survey_equiv_gbs": ALEX_BYTES_PER_CELL * E * N * N / kern / 1e9,
         "fires_left": int((env.counts[:, 2] > 0).sum().item()),
     }
+    # the full reference env step: + the RGB observation (gca_adv_observation, 12 B/cell of f32 RGB
+    # written), extension choice 1 (unblur) in every env
+    action3 = torch.zeros((E, 3), dtype=torch.int32, device=device)
+    action3[:, 2] = 1
+
+    def step_rgb(events):
+        step(None)
+        if events is not None:
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            env.render_observation(action3)
+            b.record()
+            events.append((a, b))
+        else:
+            env.render_observation(action3)
+
+    dt_rgb, kern_rgb = timed_loop(step_rgb, args.steps, args.warmup, pg, device)
+    res["with_rgb_observation"] = {"env_steps_per_s": world * E * args.steps / dt_rgb,
+                                   "cell_updates_per_s": world * E * N * N * args.steps / dt_rgb,
+                                   "obs_kernel_ms": kern_rgb * 1e3,
+                                   "obs_gbs": 14 * E * N * N / kern_rgb / 1e9,
+                                   "note": "RGB f32 observation per step like the reference's stateless_step"}
     # the same env from its reset state (two burning cells per env, advanced_bulldozer.py:650-688): a
     # real episode's first steps, where the fire-sparsity skip leaves most waves the 7 B/cell of
     # grid/age/dousing traffic. Reported separately; the headline above is the dense mid-episode state.
@@ -503,6 +526,7 @@ def main():
                                                                   if world > 1 and args.gather == "step" else "")},
             "env_steps_per_s": alex["env_steps_per_s"],
             "episode_start": alex["episode_start"],
+            "with_rgb_observation": alex["with_rgb_observation"],
             "roofline": {"bound": "hbm", "achieved": alex["achieved_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": alex["achieved_gbs"] / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "alex_step_kernel" + ("<ES>" if args.slope_layout == "edge" else ""),

@@ -4,15 +4,18 @@
 //            apply_extensions (bulldozer/utils/extension_utils.py:89-196), the reset observation
 //            (advanced_bulldozer.py:401-411).
 //
-// One workgroup per env (256 threads stride over the columns of each row), two phases:
+// Grid: one workgroup (256 threads) per (env, block of up to 16 rows):
 //   A. (step mode, only when an extension channel can be non-zero) the first row holding a positive
 //      extension value — the reference's `has_extension` is a vmap over the ROWS of the channel-last
 //      (H, W, 3 + n_ext) stack, and the row index found is then used as the channel index (clamped to
-//      the last channel, like JAX's out-of-bounds gather);
-//   B. the display value of every cell, then its f32 RGB: empty/tree/fire colour of the pre-step
-//      day/night, the water tint blended in where dousing_count == 1 (rgb*0.25 + tint*0.75 — exact in
-//      f32 for these integer colours, so the order of the reference's ops cannot matter), the
-//      position colour on the bulldozer's cell. Optionally the u8 channel stack itself.
+//      the last channel, like JAX's out-of-bounds gather). Every block of the env repeats this scan;
+//      it normally ends at row 0;
+//   B. the block's rows (+1 halo row each side) staged in LDS for the blur, then per cell the display
+//      value and its f32 RGB: empty/tree/fire colour of the pre-step day/night, the water tint blended
+//      in where dousing_count == 1 (rgb*0.25 + tint*0.75 — exact in f32 for these integer colours, so
+//      the order of the reference's ops cannot matter), the position colour on the bulldozer's cell;
+//      4 cells per thread, 3 float4 stores. Optionally the u8 channel stack itself.
+// HBM bytes per cell: grid 1 + dousing 1 read, 12 written (14 B/cell).
 // Cell transforms (values are the env's integer codes):
 //   blur(g)[r,c] = round(S / 9), S = 3x3 sum with edge padding (the reference's f32 sum of
 //   (1/9)*(g/3) times 3 is S/9 to within 1e-6 relative; S/9 is never within 0.05 of a .5 tie for
@@ -20,23 +23,31 @@
 //   vis(v) = (v == 3 && !is_night) ? 0 : v   (the reference's literal 3, extension_utils.py:93).
 #include "gca_common.h"
 
+#ifndef GCA_OBS_NT
+#define GCA_OBS_NT 1  // non-temporal RGB stores (r01i A/B: 1.07 vs 1.10 ms per 4096 x 256^2)
+#endif
+
 namespace {
 
-struct ObsCell {
-    int base;     // channel 0
-    int ext[GCA_OBS_MAX_EXT];
-};
-
+// blur of cell (lr, c) from the LDS copy of the block's rows (staged row lr+1 <-> grid row r), edge padding
+__device__ __forceinline__ int blur_lds(const uint8_t* __restrict__ T, int W, int lr, int c) {
+    int s = 0;
+#pragma unroll
+    for (int dr = 0; dr < 3; ++dr) {
+        const uint8_t* row = T + (lr + dr) * W;
+#pragma unroll
+        for (int dc = -1; dc <= 1; ++dc) s += row[min(max(c + dc, 0), W - 1)];
+    }
+    return (2 * s + 9) / 18;
+}
+// the same from global memory (display selection scan)
 __device__ __forceinline__ int blur_at(const uint8_t* __restrict__ g, int H, int W, int r, int c) {
     int s = 0;
 #pragma unroll
     for (int dr = -1; dr <= 1; ++dr) {
         const int rr = min(max(r + dr, 0), H - 1);
 #pragma unroll
-        for (int dc = -1; dc <= 1; ++dc) {
-            const int cc = min(max(c + dc, 0), W - 1);
-            s += g[(int64_t)rr * W + cc];
-        }
+        for (int dc = -1; dc <= 1; ++dc) s += g[(int64_t)rr * W + min(max(c + dc, 0), W - 1)];
     }
     return (2 * s + 9) / 18;
 }
@@ -47,19 +58,15 @@ __device__ __forceinline__ int transform(int raw, int blurred, bool night, int s
     return v;
 }
 
-__device__ __forceinline__ ObsCell cell_channels(const gca_obs_params& p, const uint8_t* __restrict__ g, int H, int W,
-                                                 int r, int c, bool night, uint32_t on) {
-    ObsCell o;
-    const int raw = g[(int64_t)r * W + c];
-    bool need_blur = p.should_transform != 0;
-    for (int i = 0; i < p.n_ext; ++i) need_blur |= ((on >> i) & 1u) && !p.ext_skip_blur[i];
-    const int bl = need_blur ? blur_at(g, H, W, r, c) : raw;
-    o.base = p.should_transform ? transform(raw, bl, night, 0, 0) : raw;
-    for (int i = 0; i < GCA_OBS_MAX_EXT; ++i)
-        o.ext[i] = (i < p.n_ext && ((on >> i) & 1u)) ? transform(raw, bl, night, p.ext_skip_visibility[i],
-                                                                   p.ext_skip_blur[i])
-                                                       : 0;
-    return o;
+struct ObsCfg {
+    bool need_blur;  // some channel in use blurs
+    uint32_t on;     // active extension channels
+    bool night;      // pre-step day/night
+};
+
+// base channel + active extension channels of one cell from its raw value and blur
+__device__ __forceinline__ int ext_value(const gca_obs_params& p, const ObsCfg& k, int i, int raw, int bl) {
+    return ((k.on >> i) & 1u) ? transform(raw, bl, k.night, p.ext_skip_visibility[i], p.ext_skip_blur[i]) : 0;
 }
 
 __device__ __forceinline__ void render(const gca_obs_params& p, float* __restrict__ out, int v, int dous, bool night,
@@ -78,81 +85,190 @@ __device__ __forceinline__ void render(const gca_obs_params& p, float* __restric
     out[2] = rgb[2];
 }
 
-__global__ __launch_bounds__(256) void adv_observation_kernel(gca_obs_params p, int mode, int H, int W,
-                                                              const uint8_t* __restrict__ grid,
+// Grid: (env, block of RB rows); 256 threads. The display selection (a scan from row 0 that normally
+// stops at the first row) is recomputed by every block of the env instead of a separate pass; the
+// block's rows plus one halo row on each side are staged in LDS for the blur; W % 4 == 0 renders
+// 4 cells per thread (3 float4 stores, 48-B aligned).
+__global__ __launch_bounds__(256) void adv_observation_kernel(gca_obs_params p, int mode, int H, int W, int RB,
+                                                              int blocks_per_env, const uint8_t* __restrict__ grid,
                                                               const uint8_t* __restrict__ dousing,
                                                               const int32_t* __restrict__ pos,
                                                               const int32_t* __restrict__ is_night,
                                                               const int32_t* __restrict__ time_step,
                                                               const int32_t* __restrict__ action, int action_stride,
                                                               float* __restrict__ rgb, uint8_t* __restrict__ channels) {
-    const int e = blockIdx.x;
+    extern __shared__ uint8_t T[];  // [(RB + 2) * W]
+    const int e = blockIdx.x / blocks_per_env;
+    const int r0 = (blockIdx.x - e * blocks_per_env) * RB;
+    const int rows = min(RB, H - r0);
     const int64_t HW = (int64_t)H * W;
     const uint8_t* g = grid + e * HW;
     const uint8_t* du = dousing ? dousing + e * HW : nullptr;
+    ObsCfg k;
     // the observation uses the PRE-step is_night; the env step toggled it when time_step % day_length == 0
-    bool night = is_night[e] != 0;
-    if (time_step && p.day_length > 0 && time_step[e] % p.day_length == 0) night = !night;
+    k.night = is_night[e] != 0;
+    if (time_step && p.day_length > 0 && time_step[e] % p.day_length == 0) k.night = !k.night;
     const int pr = pos[2 * e], pc = pos[2 * e + 1];
-    uint32_t on = 0u;
+    k.on = 0u;
     if (mode == 0 && p.enable_extensions && action && action_stride >= 3 && p.n_choices > 0) {
         const int choice = min(max(action[(int64_t)e * action_stride + 2], 0), min(p.n_choices, 8) - 1);
-        for (int i = 0; i < p.n_ext; ++i) on |= (p.ext_lookup[choice][i] != 0 ? 1u : 0u) << i;
+        for (int i = 0; i < p.n_ext; ++i) k.on |= (p.ext_lookup[choice][i] != 0 ? 1u : 0u) << i;
     }
+    k.need_blur = mode == 0 && p.should_transform != 0;
+    for (int i = 0; i < p.n_ext; ++i) k.need_blur |= ((k.on >> i) & 1u) && !p.ext_skip_blur[i];
     const int nch = 3 + p.n_ext;
 
-    // ---- A: display selection
-    int sel = -1;  // -1: the base channel; else the extension channel shown everywhere (mode 0)
-    int col_sel = 0;  // mode 1: the column of the raw grid shown (3 + clamped first row), or 0
-    if (mode == 0 && on) {
+    // ---- display selection (see the header comment in include/gca.h)
+    int sel = -1;     // mode 0: -1 = base channel, else the extension channel shown everywhere
+    int col_sel = 0;  // mode 1: column of the raw grid shown
+    if (mode == 0 && k.on) {
+        bool scan_blur = false;
+        for (int i = 0; i < p.n_ext; ++i) scan_blur |= ((k.on >> i) & 1u) && !p.ext_skip_blur[i];
         int fv = -1;
         for (int r = 0; r < H && fv < 0; ++r) {
             int any = 0;
             for (int c = threadIdx.x; c < W; c += blockDim.x) {
-                const ObsCell o = cell_channels(p, g, H, W, r, c, night, on);
-                for (int i = 0; i < p.n_ext; ++i) any |= o.ext[i] > 0;
+                const int raw = g[(int64_t)r * W + c];
+                const int bl = scan_blur ? blur_at(g, H, W, r, c) : raw;
+                for (int i = 0; i < p.n_ext; ++i) any |= ext_value(p, k, i, raw, bl) > 0;
             }
             if (__syncthreads_or(any)) fv = r;
         }
         if (fv >= 0) sel = min(fv, p.n_ext - 1);
     } else if (mode == 1 && W > 3) {
         int fv = -1;
-        for (int r0 = 0; r0 < H && fv < 0; r0 += blockDim.x) {
-            const int r = r0 + (int)threadIdx.x;
+        for (int r = 0; r < H && fv < 0; ++r) {
             int any = 0;
-            if (r < H)
-                for (int c = 3; c < W && !any; ++c) any = g[(int64_t)r * W + c] > 0;
-            // first row of this block of rows with a positive value
-            __shared__ int first;
-            if (threadIdx.x == 0) first = H;
-            __syncthreads();
-            if (any) atomicMin(&first, r);
-            __syncthreads();
-            if (first < H) fv = first;
-            __syncthreads();
+            for (int c = 3 + threadIdx.x; c < W; c += blockDim.x) any |= g[(int64_t)r * W + c] > 0;
+            if (__syncthreads_or(any)) fv = r;
         }
         col_sel = fv >= 0 ? 3 + min(fv, W - 4) : 0;
     }
 
-    // ---- B: render
-    for (int r = 0; r < H; ++r) {
-        for (int c = threadIdx.x; c < W; c += blockDim.x) {
+    if (mode == 1) {  // rgb[r][c] = colour(grid[c][col_sel]) (+ dousing of (r, c), position)
+        for (int idx = threadIdx.x; idx < rows * W; idx += blockDim.x) {
+            const int lr = idx / W, c = idx - lr * W, r = r0 + lr;
             const int64_t cell = (int64_t)r * W + c;
-            int v;
-            if (mode == 1) {
-                v = g[(int64_t)c * W + col_sel];  // display[c] (square grids, checked on the host)
-            } else {
-                const ObsCell o = cell_channels(p, g, H, W, r, c, night, on);
-                v = sel < 0 ? o.base : o.ext[sel];
-                if (channels) {
-                    uint8_t* ch = channels + (e * HW + cell) * nch;
-                    ch[0] = (uint8_t)o.base;
-                    ch[1] = 0;
-                    ch[2] = 0;
-                    for (int i = 0; i < p.n_ext; ++i) ch[3 + i] = (uint8_t)o.ext[i];
+            render(p, rgb + (e * HW + cell) * 3, g[(int64_t)c * W + col_sel], du ? du[cell] : 0, k.night,
+                   r == pr && c == pc);
+        }
+        return;
+    }
+
+    // ---- stage rows [r0 - 1, r0 + rows] (clamped: edge padding) for the blur
+    if (k.need_blur) {
+        if ((W & 3) == 0) {
+            const int wq = W >> 2;
+            for (int idx = threadIdx.x; idx < (rows + 2) * wq; idx += blockDim.x) {
+                const int lr = idx / wq, cq = idx - lr * wq;
+                const int r = min(max(r0 - 1 + lr, 0), H - 1);
+                reinterpret_cast<uint32_t*>(T)[lr * wq + cq] =
+                    reinterpret_cast<const uint32_t*>(g + (int64_t)r * W)[cq];
+            }
+        } else {
+            for (int idx = threadIdx.x; idx < (rows + 2) * W; idx += blockDim.x) {
+                const int lr = idx / W, c = idx - lr * W;
+                T[idx] = g[(int64_t)min(max(r0 - 1 + lr, 0), H - 1) * W + c];
+            }
+        }
+        __syncthreads();
+    }
+
+    auto values_of = [&](int raw, int bl, int* extv) -> int {
+        const int base = p.should_transform ? transform(raw, bl, k.night, 0, 0) : raw;
+        for (int i = 0; i < GCA_OBS_MAX_EXT; ++i) extv[i] = i < p.n_ext ? ext_value(p, k, i, raw, bl) : 0;
+        return base;
+    };
+    auto cell_value = [&](int lr, int c, int raw, int* extv) -> int {
+        return values_of(raw, k.need_blur ? blur_lds(T, W, lr, c) : raw, extv);
+    };
+    if ((W & 3) == 0) {
+        // 256 threads x 4 cells per round; the 12 floats of each thread go through LDS so that every store
+        // instruction writes 1 KiB of contiguous RGB (the rows of a block are contiguous in HBM)
+        __shared__ float4 OUT4[256 * 3];
+        const int wq = W >> 2;
+        for (int base_q = 0; base_q < rows * wq; base_q += 256) {
+            const int idx = base_q + (int)threadIdx.x;
+            if (idx < rows * wq) {
+                const int lr = idx / wq, c0 = (idx - lr * wq) * 4, r = r0 + lr;
+                const int64_t cell0 = (int64_t)r * W + c0;
+                const uint32_t gw = *reinterpret_cast<const uint32_t*>(g + cell0);
+                const uint32_t dw = du ? *reinterpret_cast<const uint32_t*>(du + cell0) : 0u;
+                // blur of the 4 cells: column sums of columns c0-1 .. c0+4 over the 3 staged rows
+                // (one aligned word + the two edge bytes per row; edge padding at the grid border)
+                int bl4[4] = {0, 0, 0, 0};
+                if (k.need_blur) {
+                    int cs[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+                    for (int dr = 0; dr < 3; ++dr) {
+                        const uint8_t* row = T + (lr + dr) * W;
+                        const uint32_t w = reinterpret_cast<const uint32_t*>(row)[c0 >> 2];
+                        cs[0] += c0 > 0 ? row[c0 - 1] : (int)(w & 0xFF);
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) cs[1 + j] += (int)((w >> (8 * j)) & 0xFF);
+                        cs[5] += c0 + 4 < W ? row[c0 + 4] : (int)(w >> 24);
+                    }
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) bl4[j] = (2 * (cs[j] + cs[j + 1] + cs[j + 2]) + 9) / 18;
+                }
+                float out[12];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int raw = (gw >> (8 * j)) & 0xFF;
+                    int extv[GCA_OBS_MAX_EXT];
+                    const int base = values_of(raw, k.need_blur ? bl4[j] : raw, extv);
+                    int v = base;
+#pragma unroll
+                    for (int i = 0; i < GCA_OBS_MAX_EXT; ++i)
+                        if (sel == i) v = extv[i];
+                    render(p, out + 3 * j, v, (dw >> (8 * j)) & 0xFF, k.night, r == pr && c0 + j == pc);
+                    if (channels) {
+                        uint8_t* ch = channels + (e * HW + cell0 + j) * nch;
+                        ch[0] = (uint8_t)base;
+                        ch[1] = 0;
+                        ch[2] = 0;
+                        for (int i = 0; i < p.n_ext; ++i) ch[3 + i] = (uint8_t)extv[i];
+                    }
+                }
+                OUT4[3 * threadIdx.x + 0] = make_float4(out[0], out[1], out[2], out[3]);
+                OUT4[3 * threadIdx.x + 1] = make_float4(out[4], out[5], out[6], out[7]);
+                OUT4[3 * threadIdx.x + 2] = make_float4(out[8], out[9], out[10], out[11]);
+            }
+            __syncthreads();
+            const int n4 = 3 * min(256, rows * wq - base_q);
+            float4* dst = reinterpret_cast<float4*>(rgb + (e * HW + (int64_t)r0 * W + 4 * (int64_t)base_q) * 3);
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                const int q4 = (int)threadIdx.x + 256 * j;
+                if (q4 < n4) {
+#if GCA_OBS_NT
+                    typedef float f4v __attribute__((ext_vector_type(4)));
+                    const float4 v = OUT4[q4];
+                    __builtin_nontemporal_store((f4v){v.x, v.y, v.z, v.w}, reinterpret_cast<f4v*>(dst + q4));
+#else
+                    dst[q4] = OUT4[q4];
+#endif
                 }
             }
-            render(p, rgb + (e * HW + cell) * 3, v, du ? du[cell] : 0, night, r == pr && c == pc);
+            __syncthreads();
+        }
+    } else {
+        for (int idx = threadIdx.x; idx < rows * W; idx += blockDim.x) {
+            const int lr = idx / W, c = idx - lr * W, r = r0 + lr;
+            const int64_t cell = (int64_t)r * W + c;
+            int extv[GCA_OBS_MAX_EXT];
+            const int base = cell_value(lr, c, g[cell], extv);
+            int v = base;
+            for (int i = 0; i < p.n_ext; ++i)
+                if (sel == i) v = extv[i];
+            render(p, rgb + (e * HW + cell) * 3, v, du ? du[cell] : 0, k.night, r == pr && c == pc);
+            if (channels) {
+                uint8_t* ch = channels + (e * HW + cell) * nch;
+                ch[0] = (uint8_t)base;
+                ch[1] = 0;
+                ch[2] = 0;
+                for (int i = 0; i < p.n_ext; ++i) ch[3 + i] = (uint8_t)extv[i];
+            }
         }
     }
 }
@@ -168,8 +284,14 @@ extern "C" int gca_adv_observation(const gca_obs_params* p, int mode, int E, int
     GCA_CHECK_ARG(p->n_ext >= 0 && p->n_ext <= GCA_OBS_MAX_EXT, "adv_observation: 0..4 extension channels");
     GCA_CHECK_ARG(mode == 0 || H == W, "adv_observation: the reset observation needs a square grid (reference broadcast)");
     GCA_CHECK_ARG(mode == 0 || channels == nullptr, "adv_observation: no channel stack in reset mode");
-    hipLaunchKernelGGL(adv_observation_kernel, dim3((unsigned)E), dim3(256), 0, (hipStream_t)stream, *p, mode, H, W,
-                       grid, dousing, pos, is_night, time_step, action, action_stride, rgb, channels);
+    GCA_CHECK_ARG(W <= 16384, "adv_observation: W <= 16384");
+    GCA_CHECK_ARG(((uintptr_t)rgb & 15u) == 0 && ((uintptr_t)grid & 3u) == 0 && ((uintptr_t)dousing & 3u) == 0,
+                  "adv_observation: rgb must be 16-B and grid/dousing 4-B aligned");
+    const int RB = max(1, min(16, 49152 / W - 2));  // rows per block; (RB + 2) * W bytes of LDS
+    const int bpe = (H + RB - 1) / RB;
+    hipLaunchKernelGGL(adv_observation_kernel, dim3((unsigned)((int64_t)E * bpe)), dim3(256), (size_t)(RB + 2) * W,
+                       (hipStream_t)stream, *p, mode, H, W, RB, bpe, grid, dousing, pos, is_night, time_step, action,
+                       action_stride, rgb, channels);
     GCA_CHECK_LAUNCH("adv_observation");
     return GCA_OK;
 }
