@@ -63,23 +63,17 @@ __device__ __forceinline__ uint32_t bfi32(uint32_t m, uint32_t a, uint32_t b) { 
 // bit i of w as an all-ones / all-zeros word (v_bfe_i32)
 __device__ __forceinline__ uint32_t sbit(uint32_t w, int i) { return (uint32_t)((int32_t)(w << (31 - i)) >> 31); }
 
-// exp_f32 (gca_common.h) on a pair: the same IEEE op sequence per half (v_pk_fma_f32 / v_pk_mul_f32 round
-// each half like the scalar op), so bit-identical with exp_f32 and the C oracle. The clamp to [-80, 80] is
-// dropped: the edge-slope exponents are 0.078 * slope with |slope| < 90 degrees (atan), |x| < 7.1.
-__device__ __forceinline__ f2 exp_f32x2(f2 x) {
-    const f2 kf = __builtin_elementwise_rint(x * (f2){1.44269504088896341f, 1.44269504088896341f});
-    f2 r = __builtin_elementwise_fma(kf, (f2){-0.693145751953125f, -0.693145751953125f}, x);
-    r = __builtin_elementwise_fma(kf, (f2){-1.42860682030941723212e-6f, -1.42860682030941723212e-6f}, r);
-    f2 p = {1.98412698412698413e-4f, 1.98412698412698413e-4f};
-    p = __builtin_elementwise_fma(p, r, (f2){1.38888888888888889e-3f, 1.38888888888888889e-3f});
-    p = __builtin_elementwise_fma(p, r, (f2){8.33333333333333333e-3f, 8.33333333333333333e-3f});
-    p = __builtin_elementwise_fma(p, r, (f2){4.16666666666666667e-2f, 4.16666666666666667e-2f});
-    p = __builtin_elementwise_fma(p, r, (f2){1.66666666666666667e-1f, 1.66666666666666667e-1f});
-    p = __builtin_elementwise_fma(p, r, (f2){0.5f, 0.5f});
-    p = __builtin_elementwise_fma(p, r * r, r);
-    p = p + (f2){1.0f, 1.0f};
-    return (f2){__uint_as_float(__float_as_uint(p.x) + ((uint32_t)(int)kf.x << 23)),
-                __uint_as_float(__float_as_uint(p.y) + ((uint32_t)(int)kf.y << 23))};
+// p_slope factors of a cell pair from edge-layout values V = +-exp_f32(|a|) (see ES below): own direction
+// (the edge's slope a): P(a) = V if V > 0 else 1/|V|; the neighbour's edge seen from the other end
+// (slope -a): P(-a) = |V| if V < 0 else 1/|V|. 1/x = recip_ge1 on the pair (packed Newton step).
+__device__ __forceinline__ f2 edge_factor_pair(float v0, float v1, bool own) {
+    const f2 x = {fabsf(v0), fabsf(v1)};
+    const f2 r0 = {__builtin_amdgcn_rcpf(x.x), __builtin_amdgcn_rcpf(x.y)};
+    const f2 ee = __builtin_elementwise_fma(-x, r0, (f2){1.0f, 1.0f});
+    const f2 rc = __builtin_elementwise_fma(ee, r0, r0);
+    const bool k0 = own ? v0 > 0.0f : v0 < 0.0f;
+    const bool k1 = own ? v1 > 0.0f : v1 < 0.0f;
+    return (f2){k0 ? x.x : rc.x, k1 ? x.y : rc.y};
 }
 // DPP moves inside a 16-lane row (= one image row of a workgroup: lanes q = 0..15)
 __device__ __forceinline__ float dpp_from_next(float old, float src) {  // lane q <- lane q+1; lane 15 keeps old
@@ -106,12 +100,15 @@ template <class T, class S> __device__ __forceinline__ T bitcast_(S s) {
 // checks and byte-wise fallbacks compile away, which also lets the waitcnt pass keep loads in flight.
 //
 // ES (edge slopes): `p_slope` is the antisymmetric edge layout of gca_alex_edge_slope_from_altitude,
-// es[e][k][r][c] = f32(raw slope of (r,c) toward neighbour k), k = 0..3 <-> (-1,-1), (-1,0), (-1,+1),
-// (0,-1) — 16 B per cell instead of 32. Direction d < 4 of cell X reads es[d][X]; d >= 4 reads
-// -es[7-d][X + off_d] (get_slope's f64 difference, division, atan and degree scaling are odd, and so is
-// the f32 cast, so slope(X -> Y) == -slope(Y -> X) exactly); p_slope = exp_f32(0.078f * slope) in-kernel,
-// and cells on the grid border get slope 0 -> p_slope = 1 (get_slope leaves their slopes 0).
-// Bit-identical to the 8-plane layout built from the same altitude (tests/test_gpu_alexandridis.py).
+// es[e][k][r][c] = V = +-exp_f32(|a|), a = 0.078f * f32(raw slope of (r,c) toward neighbour k),
+// k = 0..3 <-> (-1,-1), (-1,0), (-1,+1), (0,-1), sign = sign of a — 16 B per cell instead of 32.
+// get_slope's f64 difference, division, atan and degree scaling are odd, and so are the f32 cast and
+// the 0.078f product, so the neighbour sees exactly -a. With p_slope = slope_factor(a) (gca_common.h:
+// exp_f32(a) for a >= 0, 1 / exp_f32(-a) otherwise), direction d < 4 of cell X is P(a) = V > 0 ? V :
+// 1/|V| and direction d >= 4 is P(-a) of the neighbour X + off_d's edge: |V| if V < 0, else 1/|V|;
+// 1/x is recip_ge1 (v_rcp_f32 + one Newton step, correctly rounded on [1, 1121], tested exhaustively).
+// Cells on the grid border get p_slope = 1 (get_slope leaves their slopes 0).
+// Bit-identical to the 8-plane layout built from the same altitude (tests/test_gpu_edge_slope.py).
 //
 // Fire sparsity (MODE 0): p_slope, vegetation, density, the heat field and the per-direction products
 // only matter for TREE cells with a burning neighbour. A workgroup with no FIRE within one cell of its tile
@@ -154,10 +151,10 @@ __global__ __launch_bounds__(256, GCA_ALEX_WGS) void alex_step_kernel(
     const uint8_t* gE = grid_in + (int64_t)e * HW;
     const uint8_t* dE = dousing + (int64_t)e * HW;
     const int tid = threadIdx.x;
-    const bool rows16 = FAST || ((W & 15) == 0) &&
-                        ((((uintptr_t)grid_in) | ((uintptr_t)dousing) | ((uintptr_t)grid_out) | ((uintptr_t)veg) |
-                          ((uintptr_t)den) | ((uintptr_t)age_in) | ((uintptr_t)age_out) | ((uintptr_t)p_slope)) &
-                         15u) == 0;
+    const bool rows16 = FAST || (((W & 15) == 0) &&
+                                 ((((uintptr_t)grid_in) | ((uintptr_t)dousing) | ((uintptr_t)grid_out) |
+                                   ((uintptr_t)veg) | ((uintptr_t)den) | ((uintptr_t)age_in) | ((uintptr_t)age_out) |
+                                   ((uintptr_t)p_slope)) & 15u) == 0);
     const uint32_t Fp = rep4((uint32_t)p.fire), Ep = rep4((uint32_t)p.empty), Tp = rep4((uint32_t)p.tree);
 
     // ---------------- this thread's 16 cells: row r, columns [cbase, cbase+16)
@@ -415,6 +412,7 @@ __global__ __launch_bounds__(256, GCA_ALEX_WGS) void alex_step_kernel(
     const float w_in_minus_bd = __fsub_rn(p.dous_inner, p.dous_border);
     auto fire_f = [](uint32_t s) -> float { return R <= 7 ? (float)(s & 0xFFu) : (float)(s & 0xFFFFu); };
     if (wave_need) {
+#ifndef GCA_ABL_NOHEAT
 #pragma unroll
         for (int k = 0; k <= RS; ++k) {
             uint32_t V[16 + 2 * RS];
@@ -452,6 +450,7 @@ __global__ __launch_bounds__(256, GCA_ALEX_WGS) void alex_step_kernel(
             for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(ph2[j]), "+v"(dz2[j]));
             __builtin_amdgcn_sched_barrier(0);
         }
+#endif
 #pragma unroll
         for (int j = 0; j < 8; ++j) ph2[j] = ph2[j] - dz2[j];  // p_h = heat - dousing (:198)
 #if GCA_ALEX_WGS >= 4
@@ -538,20 +537,20 @@ __global__ __launch_bounds__(256, GCA_ALEX_WGS) void alex_step_kernel(
                     for (int i = 15; i > 0; --i) a[i] = a[i - 1];
                     a[0] = pv;
                 }
+                // border cells: factor +1 (slope 0 -> p_slope = 1 either way round)
                 if (wave_rowkill) {
 #pragma unroll
-                    for (int i = 0; i < 16; ++i) a[i] = rowkill ? 0.0f : a[i];
+                    for (int i = 0; i < 16; ++i) a[i] = rowkill ? 1.0f : a[i];
                 }
-                a[0] = kill_lo ? 0.0f : a[0];
+                a[0] = kill_lo ? 1.0f : a[0];
                 if (FAST) {
-                    a[15] = hi_idx == 15 ? 0.0f : a[15];
+                    a[15] = hi_idx == 15 ? 1.0f : a[15];
                 } else {
 #pragma unroll
-                    for (int i = 0; i < 16; ++i) a[i] = hi_idx == i ? 0.0f : a[i];
+                    for (int i = 0; i < 16; ++i) a[i] = hi_idx == i ? 1.0f : a[i];
                 }
-                const float sg = d < 4 ? 0.078f : -0.078f;  // d >= 4: -es of the neighbour (exact negation)
 #pragma unroll
-                for (int j = 0; j < 8; ++j) ps2[j] = exp_f32x2((f2){sg, sg} * (f2){a[2 * j], a[2 * j + 1]});
+                for (int j = 0; j < 8; ++j) ps2[j] = edge_factor_pair(a[2 * j], a[2 * j + 1], d < 4);
             }
             // pin base here: otherwise the 64 direction-independent products base*wind[d] are hoisted
             // above the loop (128 live VGPRs -> spills)
@@ -630,7 +629,11 @@ __global__ __launch_bounds__(256, GCA_ALEX_WGS) void alex_step_kernel(
             u32x4 XA = u32x4{0u, 0u, 0u, 0u}, XB = u32x4{0u, 0u, 0u, 0u};
             uint32_t m0, m1, a0, a1;
             if (!odd) {
+#ifdef GCA_ABL_NOPHILOX
+                if (nd) XA = u32x4{cA * 0x9E3779B9u, env_id ^ cA, step + cA, cA};
+#else
                 if (nd) XA = philox4x32_10(u32x4{cA, env_id, step, GCA_TAG_ALEX_CELL}, k0, k1);
+#endif
                 m0 = XA.x; a0 = XA.y; m1 = XA.z; a1 = XA.w;
             } else {
                 if (nd & 1u) XA = philox4x32_10(u32x4{cA, env_id, step, GCA_TAG_ALEX_CELL}, k0, k1);
@@ -730,7 +733,7 @@ __global__ __launch_bounds__(256, GCA_ALEX_WGS) void alex_step_kernel(
     }
 }
 
-// p_slope[e][d][r][c] = exp_f32(0.078f * slope[e][r][c][d'])
+// p_slope[e][d][r][c] = slope_factor(0.078f * slope[e][r][c][d'])
 __global__ void alex_prepare_slope_kernel(const float* __restrict__ slope, float* __restrict__ p_slope, int64_t HW,
                                           int E) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -741,7 +744,7 @@ __global__ void alex_prepare_slope_kernel(const float* __restrict__ slope, float
 #pragma unroll
     for (int d = 0; d < 8; ++d) {
         const float a = __fmul_rn(0.078f, s[d < 4 ? d : d + 1]);
-        p_slope[((int64_t)e * 8 + d) * HW + cell] = exp_f32(a);
+        p_slope[((int64_t)e * 8 + d) * HW + cell] = slope_factor(a);
     }
 }
 
@@ -871,15 +874,15 @@ __global__ void alex_slope_from_altitude_kernel(const double* __restrict__ alt, 
             }
             if (slope_out) slope_out[idx * 9 + 3 * i + j] = s;
             if (i == 1 && j == 1) continue;
-            p_slope[((int64_t)e * 8 + d) * HW + cell] = exp_f32(__fmul_rn(0.078f, s));
+            p_slope[((int64_t)e * 8 + d) * HW + cell] = slope_factor(__fmul_rn(0.078f, s));
             ++d;
         }
     }
 }
 }  // namespace
 
-// Edge layout of the same slopes (see alex_step_kernel, ES): es[e][k][r][c] = f32(raw slope of
-// (r,c) toward neighbour k), k = 0..3 <-> (-1,-1), (-1,0), (-1,+1), (0,-1), with get_slope's arithmetic
+// Edge layout of the same slopes (see alex_step_kernel, ES): es[e][k][r][c] = the signed slope factor
+// of (r,c) toward neighbour k (+exp_f32(a) for a >= 0, -exp_f32(-a) for a < 0, a = 0.078f * f32(raw slope)), k = 0..3 <-> (-1,-1), (-1,0), (-1,+1), (0,-1), with get_slope's arithmetic
 // but WITHOUT its border zeroing (the step kernel applies that per cell); 0 where the neighbour is outside.
 namespace {
 __global__ void alex_edge_slope_from_altitude_kernel(const double* __restrict__ alt, float* __restrict__ es, int H,
@@ -901,10 +904,37 @@ __global__ void alex_edge_slope_from_altitude_kernel(const double* __restrict__ 
             if (dr != 0 && dc != 0) diff /= 1.414;
             s = (float)(atan(diff) * (180.0 / 3.14159265358979323846));
         }
-        es[((int64_t)e * 4 + k) * HW + cell] = s;
+        // signed factor: +exp_f32(a) for a >= 0, -exp_f32(-a) for a < 0, a = 0.078f * slope
+        const float a = __fmul_rn(0.078f, s);
+        es[((int64_t)e * 4 + k) * HW + cell] = a >= 0.0f ? exp_f32(a) : -exp_f32(-a);
     }
 }
 }  // namespace
+
+namespace {
+__global__ void alex_edge_factors_kernel(const float* __restrict__ v, float* __restrict__ own, float* __restrict__ nbr,
+                                         int64_t n) {
+    const int64_t i = 2 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+    if (i >= n) return;
+    const float v0 = v[i], v1 = i + 1 < n ? v[i + 1] : 1.0f;
+    const f2 o = edge_factor_pair(v0, v1, true), b = edge_factor_pair(v0, v1, false);
+    own[i] = o.x;
+    nbr[i] = b.x;
+    if (i + 1 < n) {
+        own[i + 1] = o.y;
+        nbr[i + 1] = b.y;
+    }
+}
+}  // namespace
+
+extern "C" int gca_alex_edge_factors(const float* v, float* own, float* nbr, int64_t n, void* stream) {
+    GCA_CHECK_ARG(v && own && nbr && n > 0, "edge_factors: bad arguments");
+    const int64_t pairs = (n + 1) / 2;
+    hipLaunchKernelGGL(alex_edge_factors_kernel, dim3((unsigned)((pairs + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, v, own, nbr, n);
+    GCA_CHECK_LAUNCH("alex_edge_factors");
+    return GCA_OK;
+}
 
 extern "C" int gca_alex_edge_slope_from_altitude(const double* altitude, float* edge_slope, int E, int H, int W,
                                                  void* stream) {

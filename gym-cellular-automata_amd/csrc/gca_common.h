@@ -113,6 +113,24 @@ __device__ __forceinline__ float exp_f32(float x) {
     return __uint_as_float(__float_as_uint(p) + ((uint32_t)k << 23));
 }
 
+// ----------------------------------------------------------------- slope factor
+// p_slope = P(a), a = 0.078f * slope (ca_alexandridis_jax.py:199-200: exp(0.078 * slope)):
+//   P(a) = exp_f32(a) for a >= 0,  1 / exp_f32(-a) (IEEE division) for a < 0.
+// Within 2 ulp of exp(a); defined through exp_f32 of |a| so that the two directions of one edge
+// (slopes s and -s) share one exp: P(-a) = 1 / P(a) exactly (the edge-slope layout stores one value
+// per edge). The C oracle restates it (oracle_slope_factor).
+__device__ __forceinline__ float slope_factor(float a) {
+    return a >= 0.0f ? exp_f32(a) : __fdiv_rn(1.0f, exp_f32(-a));
+}
+// 1 / x correctly rounded for x in [1, 2048): v_rcp_f32 (<= 1 ulp) + one Newton step in fma.
+// Verified against IEEE division for every f32 in [1, 1121] (tests/test_gpu_edge_slope.py), the range
+// of exp_f32(|0.078 * slope|) for |slope| < 90 degrees.
+__device__ __forceinline__ float recip_ge1(float x) {
+    const float r0 = __builtin_amdgcn_rcpf(x);
+    const float e = fmaf(-x, r0, 1.0f);
+    return fmaf(e, r0, r0);
+}
+
 // ----------------------------------------------------------------- SWAR byte helpers
 // Per-byte equality with a replicated pattern: returns 0x01 in each byte where x == pat.
 __device__ __forceinline__ uint32_t bytes_eq01(uint32_t x, uint32_t pat) {

@@ -137,6 +137,7 @@ _SIGNATURES = {
     "gca_alex_step_es": ([POINTER(AlexParams), c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
                          c_int),
     "gca_alex_edge_slope_from_altitude": ([P, P, c_int, c_int, c_int, P], c_int),
+    "gca_alex_edge_factors": ([P, P, P, c_int64, P], c_int),
     "gca_adv_observation": ([POINTER(ObsParams), c_int, c_int, c_int, c_int, P, P, P, P, P, P, c_int, P, P, P],
                             c_int),
     "gca_alex_altitude_apply": ([P, c_int, c_int, c_int, P, P, P, P, P], c_int),

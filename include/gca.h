@@ -135,8 +135,9 @@ typedef struct {
                                   ca_alexandridis.py:181-183). Ages are decremented either way. */
 } gca_alex_params;
 
-/* p_slope[e][d][r][c] = exp_f32(0.078f * slope[e][r][c][d']) for the 8 non-centre d'
- * (ca_alexandridis_jax.py:199-200). exp_f32 is the deterministic expf of DESIGN.md. */
+/* p_slope[e][d][r][c] = slope_factor(0.078f * slope[e][r][c][d']) for the 8 non-centre d'
+ * (ca_alexandridis_jax.py:199-200: exp(0.078 * slope)); slope_factor(a) = exp_f32(a) for a >= 0 and
+ * 1 / exp_f32(-a) for a < 0 (IEEE division), exp_f32 the deterministic expf of DESIGN.md. */
 int gca_alex_prepare_slope(const float* slope, float* p_slope, int E, int H, int W, void* stream);
 
 /* One CA step of PartiallyObservableForestFireJax._update_grid (ca_alexandridis_jax.py:321-424).
@@ -164,10 +165,15 @@ int gca_alex_step_es(const gca_alex_params* p, int E, int H, int W, const uint8_
                      float* prob_out, int32_t* counts, void* stream);
 
 /* Edge-slope layout for gca_alex_step_es from altitude [E][H][W] f64 (NULL = flat): edge_slope[e][k][r][c] =
- * f32(degrees(atan((alt[r][c] - alt[n]) / (1.414 if diagonal)))) toward neighbour n = k-th of
- * (-1,-1), (-1,0), (-1,+1), (0,-1) (0 where n is outside the grid), i.e. get_slope (init_utils.py:166-200)
- * without its border zeroing, which the step applies per cell.                                        */
+ * V = +exp_f32(a) if a >= 0 else -exp_f32(-a), a = 0.078f * s, s = f32(degrees(atan((alt[r][c] - alt[n]) /
+ * (1.414 if diagonal)))) toward neighbour n = k-th of (-1,-1), (-1,0), (-1,+1), (0,-1) (s = 0 where n is
+ * outside the grid): get_slope (init_utils.py:166-200) without its border zeroing, which the step applies
+ * per cell. p_slope everywhere is slope_factor(a) = exp_f32(a) (a >= 0) or 1/exp_f32(-a) (a < 0), so
+ * both directions of an edge come from V: P(a) = V > 0 ? V : 1/|V|, P(-a) = V < 0 ? |V| : 1/|V|.      */
 int gca_alex_edge_slope_from_altitude(const double* altitude, float* edge_slope, int E, int H, int W, void* stream);
+/* (own, neighbour) factors the step derives from n edge values V, with the step's own arithmetic
+ * (v_rcp_f32 + Newton reciprocal): the hook the exhaustive reciprocal test calls.                   */
+int gca_alex_edge_factors(const float* v, float* own, float* nbr, int64_t n, void* stream);
 
 /* Wind change of PartiallyObservableForestFireJax.update (ca_alexandridis_jax.py:442-451) for E envs:
  * u < p_wind_change -> wind_index = (wind_index + k) % n_winds, k in [1, 8).

@@ -34,6 +34,8 @@ def lib():
         _lib = ctypes.CDLL(LIB)
         _lib.oracle_exp_f32.restype = ctypes.c_float
         _lib.oracle_exp_f32.argtypes = [ctypes.c_float]
+        _lib.oracle_slope_factor.restype = ctypes.c_float
+        _lib.oracle_slope_factor.argtypes = [ctypes.c_float]
     return _lib
 
 
@@ -59,6 +61,28 @@ def exp_f32(x):
     f = lib().oracle_exp_f32
     return np.array([f(float(v)) for v in np.asarray(x, dtype=np.float32).ravel()], dtype=np.float32).reshape(
         np.shape(x))
+
+
+def slope_factor(a):
+    f = lib().oracle_slope_factor
+    return np.array([f(float(v)) for v in np.asarray(a, dtype=np.float32).ravel()], dtype=np.float32).reshape(
+        np.shape(a))
+
+
+def signed_factors(slope):
+    """Edge-layout values V = +-exp_f32(|0.078 * slope|) (sign of the slope) for an f32 slope array."""
+    slope = np.ascontiguousarray(slope, dtype=np.float32)
+    out = np.empty_like(slope)
+    lib().oracle_signed_factors(_p(slope), _p(out), ctypes.c_long(slope.size))
+    return out
+
+
+def factor_pairs(v):
+    """(own, neighbour) slope factors the edge-slope kernel derives from V."""
+    v = np.ascontiguousarray(v, dtype=np.float32)
+    own, nbr = np.empty_like(v), np.empty_like(v)
+    lib().oracle_factor_pairs(_p(v), _p(own), _p(nbr), ctypes.c_long(v.size))
+    return own, nbr
 
 
 def prepare_slope(slope):

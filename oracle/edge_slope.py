@@ -7,11 +7,14 @@ gca_alex_step_es expands it, so the CPU suite can pin the layout against get_slo
     edge[e][k][r][c] = f32(degrees(arctan((alt[r,c] - alt[n]) / (1.414 if diagonal))))
         n = (r,c) + OFF[k], OFF = (-1,-1), (-1,0), (-1,+1), (0,-1); 0 where n is outside the grid
         (no border zeroing: a border cell's slope toward an interior one is still needed by that one)
+    (the device stores edge_values(edge) = +-exp_f32(|0.078 s|), see oracle_signed_factors)
     slope9[r,c,(i,j)] = edge[k][r,c]           for (i-1, j-1) = OFF[k]
                       = -edge[k][(r,c)-OFF[k]] for (i-1, j-1) = -OFF[k]
                       = 0 on the grid border and at the centre (get_slope's zero border).
 """
 import numpy as np
+
+from . import alex_c
 
 OFF = ((-1, -1), (-1, 0), (-1, 1), (0, -1))
 
@@ -58,3 +61,8 @@ def slope9_from_edge(edge):
     s9[:, :, -1] = 0
     s9[..., 1, 1] = 0
     return s9
+
+
+def edge_values(edge_slopes):
+    """The device's stored edge values V = +-exp_f32(|0.078 * s|) (sign of s) of (E, 4, H, W) slopes."""
+    return alex_c.signed_factors(edge_slopes)

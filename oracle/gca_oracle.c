@@ -91,13 +91,35 @@ float oracle_exp_f32(float x) {
     return y;
 }
 
+/* p_slope factor of a = 0.078f * slope (device slope_factor, gca_common.h): exp_f32(a) for a >= 0,
+ * 1 / exp_f32(-a) (IEEE division) for a < 0 — so the two directions of one edge are exact reciprocals */
+float oracle_slope_factor(float a) { return a >= 0.0f ? oracle_exp_f32(a) : 1.0f / oracle_exp_f32(-a); }
+
+/* the edge layout's signed factor V = +exp_f32(a) (a >= 0) / -exp_f32(-a) (a < 0), a = 0.078f * slope */
+void oracle_signed_factors(const float* slope, float* v, long n) {
+    for (long i = 0; i < n; ++i) {
+        const float a = 0.078f * slope[i];
+        v[i] = a >= 0.0f ? oracle_exp_f32(a) : -oracle_exp_f32(-a);
+    }
+}
+
+/* the factor of the neighbour direction from V (the kernel's rule): P(-a) = |V| if V < 0 else 1/|V|,
+ * and the own direction P(a) = V if V > 0 else 1/|V| */
+void oracle_factor_pairs(const float* v, float* own, float* nbr, long n) {
+    for (long i = 0; i < n; ++i) {
+        const float x = fabsf(v[i]);
+        own[i] = v[i] > 0.0f ? x : 1.0f / x;
+        nbr[i] = v[i] < 0.0f ? x : 1.0f / x;
+    }
+}
+
 void oracle_alex_prepare_slope(const float* slope, float* p_slope, int E, int H, int W) {
     const long HW = (long)H * W;
     for (int e = 0; e < E; ++e)
         for (long cell = 0; cell < HW; ++cell)
             for (int d = 0; d < 8; ++d) {
                 const float s = slope[((long)e * HW + cell) * 9 + (d < 4 ? d : d + 1)];
-                p_slope[((long)e * 8 + d) * HW + cell] = oracle_exp_f32(0.078f * s);
+                p_slope[((long)e * 8 + d) * HW + cell] = oracle_slope_factor(0.078f * s);
             }
 }
 

@@ -77,14 +77,52 @@ SIZES = [(2, 5, 7, 1), (2, 16, 16, 2), (3, 37, 45, 3), (2, 64, 64, 4), (1, 100, 
 
 @pytest.mark.parametrize("E,H,W,seed", SIZES)
 def test_edge_device_layout_matches_restatement(device, E, H, W, seed):
+    import torch
+
+    from gymca_amd import _device as dev
+    from gymca_amd._lib import call
+
     alt = altitude(E, H, W, seed)
     es, ps = slopes(device, alt)
-    got9 = edge_slope.slope9_from_edge(es.cpu().numpy())
-    # the device's own 8-plane slopes, expanded from its edge layout, give its 8-plane p_slope exactly
-    assert np.array_equal(alex_c.prepare_slope(got9.reshape(E, H, W, 9)), ps.cpu().numpy())
-    # and the edge values agree with numpy's arctan to the ulp (device vs host atan)
-    want = edge_slope.edge_from_altitude(alt)
-    assert np.allclose(es.cpu().numpy(), want, rtol=2e-7, atol=1e-12)
+    es = es.cpu().numpy()
+    # the device's own f32 slopes (get_slope with its border zeroing) -> the oracle's edge values: equal
+    # bit for bit on interior cells (the same f32 slope, exp_f32 and sign rule)
+    a = _t(alt, torch.float64, device)
+    s9 = torch.empty((E, H, W, 3, 3), dtype=torch.float32, device=device)
+    tmp = torch.empty((E, 8, H, W), dtype=torch.float32, device=device)
+    call("gca_alex_slope_from_altitude", dev.ptr(a), dev.ptr(tmp), dev.ptr(s9), E, H, W, dev.stream_ptr())
+    s9 = s9.cpu().numpy()
+    own = np.stack([s9[:, :, :, 0, 0], s9[:, :, :, 0, 1], s9[:, :, :, 0, 2], s9[:, :, :, 1, 0]], axis=1)
+    if H > 2 and W > 2:
+        want = edge_slope.edge_values(own)
+        assert np.array_equal(es[:, :, 1:-1, 1:-1], want[:, :, 1:-1, 1:-1])
+    # all cells (borders too) against the host restatement, to the ulp of numpy's vs the device's atan
+    host = edge_slope.edge_values(edge_slope.edge_from_altitude(alt))
+    assert np.allclose(es, host, rtol=3e-6, atol=0)
+
+
+def test_edge_factor_reciprocal_exhaustive(device):
+    """The kernel's v_rcp_f32 + Newton reciprocal equals IEEE division for EVERY f32 in [1, 1121] (the range of
+    exp_f32(|0.078 slope|), |slope| < 90), both signs, own and neighbour directions."""
+    import torch
+
+    from gymca_amd import _device as dev
+    from gymca_amd._lib import call
+
+    lo = np.float32(1.0).view(np.uint32)
+    hi = np.float32(1121.0).view(np.uint32)
+    chunk = 1 << 24
+    for start in range(int(lo), int(hi) + 1, chunk):
+        bits = np.arange(start, min(start + chunk, int(hi) + 1), dtype=np.uint32)
+        x = bits.view(np.float32)
+        for v in (x, -x):
+            vd = torch.as_tensor(v, device=device)
+            own, nbr = torch.empty_like(vd), torch.empty_like(vd)
+            call("gca_alex_edge_factors", dev.ptr(vd), dev.ptr(own), dev.ptr(nbr), v.size, dev.stream_ptr())
+            inv = (np.float32(1) / x).astype(np.float32)
+            want_own, want_nbr = (x, inv) if v[0] > 0 else (inv, x)
+            assert np.array_equal(own.cpu().numpy(), want_own)
+            assert np.array_equal(nbr.cpu().numpy(), want_nbr)
 
 
 @pytest.mark.parametrize("E,H,W,seed", SIZES)

@@ -33,3 +33,21 @@ def test_exp_f32_accuracy_one_ulp():
     ulp = np.spacing(ref.astype(np.float32)).astype(np.float64)
     assert np.max(np.abs(y - ref) / ulp) <= 1.0
     assert alex_c.exp_f32(np.float32(0.0)) == 1.0
+
+
+def test_slope_factor_accuracy_and_reciprocity():
+    """p_slope = slope_factor(a): exp_f32(a) for a >= 0, 1/exp_f32(-a) below 0 — within 2 ulp of exp and
+    the two directions of an edge are exact reciprocals (what the edge-slope layout relies on)."""
+    a = (np.float32(0.078) * np.linspace(-90, 90, 20001).astype(np.float32)).astype(np.float32)
+    y = alex_c.slope_factor(a)
+    ref = np.exp(a.astype(np.float64))
+    ulp = np.spacing(ref.astype(np.float32)).astype(np.float64)
+    assert np.max(np.abs(y - ref) / ulp) <= 2.0
+    pos = a[a > 0]
+    assert np.array_equal(alex_c.slope_factor(-pos), (np.float32(1) / alex_c.slope_factor(pos)).astype(np.float32))
+    # the edge layout: V from the slope, then both directions from V alone
+    s = np.linspace(-89.9, 89.9, 4001).astype(np.float32)
+    own, nbr = alex_c.factor_pairs(alex_c.signed_factors(s))
+    a = (np.float32(0.078) * s).astype(np.float32)
+    assert np.array_equal(own, alex_c.slope_factor(a))
+    assert np.array_equal(nbr, alex_c.slope_factor(-a))
