@@ -5,7 +5,7 @@
 set -e
 NAME=$1; shift
 R=$(cd "$(dirname "$0")/.." && pwd)
-C=$R/gym-cellular-automata_amd/csrc
+C=${VARIANT_SRC:-$R/gym-cellular-automata_amd/csrc}  # VARIANT_SRC: another source tree (e.g. a git worktree)
 O=$R/gym-cellular-automata_amd/gymca_amd/_lib/variants
 B=$C/build/variant_$NAME
 mkdir -p $O $B
