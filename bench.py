@@ -47,6 +47,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--slope-layout", choices=["edge", "planes"], default="edge")
+    ap.add_argument("--headline-only", action="store_true",
+                    help="only the headline loop (no RGB / episode-start loops): every alex_step launch is the "
+                         "dense mid-episode one, so rocprofv3 per-kernel averages match kernel_ms")
     return ap.parse_args()
 
 
@@ -159,6 +162,8 @@ def bench_alex(args, world, rank, device, pg):
         "survey_equiv_gbs": ALEX_BYTES_PER_CELL * E * N * N / kern / 1e9,
         "fires_left": int((env.counts[:, 2] > 0).sum().item()),
     }
+    if args.headline_only:
+        return res
     # the full reference env step: + the RGB observation (gca_adv_observation, 12 B/cell of f32 RGB
     # written), extension choice 1 (unblur) in every env
     action3 = torch.zeros((E, 3), dtype=torch.int32, device=device)
@@ -525,15 +530,21 @@ def main():
                        "parallelism": f"env-sharded x{world}" + (", RCCL all_gather done/reward per step"
                                                                   if world > 1 and args.gather == "step" else "")},
             "env_steps_per_s": alex["env_steps_per_s"],
-            "episode_start": alex["episode_start"],
-            "with_rgb_observation": alex["with_rgb_observation"],
-            "roofline": {"bound": "hbm", "achieved": alex["achieved_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": alex["achieved_gbs"] / HBM_PEAK_GBS, "traffic": traffic,
+            "episode_start": alex.get("episode_start"),
+            "with_rgb_observation": alex.get("with_rgb_observation"),
+            # achieved = SURVEY.md §8d's algorithmic figure (41 B per cell-update, "independent of the build's
+            # actual layout") x cells / the kernel's mean launch time; the bytes this build actually moves
+            # (edge-slope layout: 25 B/cell) and the PMC traffic are reported beside it
+            "roofline": {"bound": "hbm", "achieved": alex["survey_equiv_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": alex["survey_equiv_gbs"] / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "alex_step_kernel" + ("<ES>" if args.slope_layout == "edge" else ""),
                          "kernel_ms": alex["kernel_ms"],
-                         "algorithmic_bytes_per_cell": ALEX_BYTES[args.slope_layout],
+                         "algorithmic_bytes_per_cell": ALEX_BYTES_PER_CELL,
                          "slope_layout": args.slope_layout,
-                         "survey_41B_equiv_gbs": alex["survey_equiv_gbs"],
+                         "moved_bytes_per_cell": ALEX_BYTES[args.slope_layout],
+                         "moved_gbs": alex["achieved_gbs"],
+                         "moved_frac": alex["achieved_gbs"] / HBM_PEAK_GBS,
+                         "traffic_bytes_per_cell": traffic / (args.envs * args.size * args.size) if traffic else None,
                          "device_copy_gbs": copy_gbs},
             "cpu_baseline": cpu,
             "secondary": secondary,

@@ -21,7 +21,8 @@ import sys
 from collections import defaultdict
 
 KERNELS = {"alex_step_kernel": "alex_step", "windy_fast_kernel": "windy_fast", "windy_exact_kernel": "windy_exact",
-           "count_kernel": "count", "advenv_post_kernel": "advenv_post"}
+           "count_kernel": "count", "advenv_post_kernel": "advenv_post",
+           "adv_observation_kernel": "adv_observation", "random_actions_kernel": "random_actions"}
 
 
 def short(name):
