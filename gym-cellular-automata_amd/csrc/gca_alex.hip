@@ -31,12 +31,13 @@ namespace {
 constexpr int TH = 16;
 constexpr int TW = 256;
 constexpr int CW = TW + 32;  // staged columns: [c0-16, c0+TW+16)
-// LDS row layout of the column prefix: one pad dword after every 16 columns (column c at
-// c + c/16) and a row stride = 16 (mod 32) dwords, so the 64 lanes of a heat-window read
-// (4 rows x 16 lanes, 16 columns apart) hit 64 distinct banks of a ds_read_b32 lane group.
-constexpr int CWP = 336;
-__host__ __device__ constexpr int pcol(int c) { return c + (c >> 4); }
-static_assert(pcol(CW - 1) < CWP && CWP % 32 == 16, "padded row");
+// LDS row layout of the column prefix: unpadded rows of CW dwords, one 16-dword chunk per 16 columns
+// (16-B aligned: the heat phase reads a lane's 16 columns as 4 x ds_read_b128). Inside chunk q, the
+// 4-column group g is stored at group slot (g + q/4) & 3: the 16 lanes of a b128 read (chunks q..q+15,
+// same g) then cover 64 distinct banks, and so do 64 consecutive columns read as b32 (prefix phase).
+constexpr int CWP = CW;
+__host__ __device__ constexpr int pcol(int c) { return 16 * (c >> 4) + 4 * ((((c >> 2) & 3) + (c >> 6)) & 3) + (c & 3); }
+static_assert(CWP % 4 == 0, "16-B aligned rows");
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
@@ -65,15 +66,28 @@ __device__ __forceinline__ uint32_t sbit(uint32_t w, int i) { return (uint32_t)(
 
 // p_slope factors of a cell pair from edge-layout values V = +-exp_f32(|a|) (see ES below): own direction
 // (the edge's slope a): P(a) = V if V > 0 else 1/|V|; the neighbour's edge seen from the other end
-// (slope -a): P(-a) = |V| if V < 0 else 1/|V|. 1/x = recip_ge1 on the pair (packed Newton step).
+// (slope -a): P(-a) = |V| if V < 0 else 1/|V|. With rc = 1/V (signed: v_rcp_f32 + one packed Newton
+// step, the exact negation of the same steps on |V|) and |V| >= 1 >= |rc|, the selections are
+// P(a) = max(V, -rc) and P(-a) = max(-V, rc): one v_max_f32 per cell instead of a compare and a select.
 __device__ __forceinline__ f2 edge_factor_pair(float v0, float v1, bool own) {
-    const f2 x = {fabsf(v0), fabsf(v1)};
-    const f2 r0 = {__builtin_amdgcn_rcpf(x.x), __builtin_amdgcn_rcpf(x.y)};
-    const f2 ee = __builtin_elementwise_fma(-x, r0, (f2){1.0f, 1.0f});
+    const f2 x = {v0, v1};
+    const f2 r0 = {__builtin_amdgcn_rcpf(v0), __builtin_amdgcn_rcpf(v1)};
+    // ee = 1 - x * r0 on both halves (neg modifiers in the instruction; the compiler sometimes emits sign
+    // xors). The s_nop covers the v_rcp_f32 (trans) -> VALU read hazard, which the hazard recogniser does
+    // not apply to inline-asm operands (without it the high half read a stale r0).
+    f2 ee;
+    asm("s_nop 1\n\tv_pk_fma_f32 %0, %1, %2, 1.0 op_sel_hi:[1,1,0] neg_lo:[1,0,0] neg_hi:[1,0,0]"
+        : "=v"(ee) : "v"(x), "v"(r0));
     const f2 rc = __builtin_elementwise_fma(ee, r0, r0);
-    const bool k0 = own ? v0 > 0.0f : v0 < 0.0f;
-    const bool k1 = own ? v1 > 0.0f : v1 < 0.0f;
-    return (f2){k0 ? x.x : rc.x, k1 ? x.y : rc.y};
+    f2 o;  // v_max_f32 with a neg source modifier (fmaxf would add canonicalising maxes and sign xors)
+    if (own) {
+        asm("v_max_f32_e64 %0, %1, -%2" : "=v"(o.x) : "v"(v0), "v"(rc.x));
+        asm("v_max_f32_e64 %0, %1, -%2" : "=v"(o.y) : "v"(v1), "v"(rc.y));
+    } else {
+        asm("v_max_f32_e64 %0, -%1, %2" : "=v"(o.x) : "v"(v0), "v"(rc.x));
+        asm("v_max_f32_e64 %0, -%1, %2" : "=v"(o.y) : "v"(v1), "v"(rc.y));
+    }
+    return o;
 }
 // DPP moves inside a 16-lane row (= one image row of a workgroup: lanes q = 0..15)
 __device__ __forceinline__ float dpp_from_next(float old, float src) {  // lane q <- lane q+1; lane 15 keeps old
@@ -297,17 +311,18 @@ __global__ __launch_bounds__(256, GCA_ALEX_WGS) void alex_step_kernel(
         const int ch = tid + 256 * it;
         if (ch >= RR * NCH) break;
         const int sr = ch / NCH, cq = ch - sr * NCH;
-        uint32_t* cp = CP + (sr + 1) * CWP + 17 * cq;  // = pcol(16 * cq)
+        uint32_t* cp = CP + (sr + 1) * CWP + 16 * cq;  // chunk cq; word j (columns 4j..4j+3) at slot (j + cq/4) & 3
         uint32_t bits = 0u;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const uint32_t f = bytes_eq01(sgw[it][j], Fp);  // 0x01 in every FIRE byte
             bits |= ((f * 0x01020408u) >> 24) << (4 * j);
-            // cell m of this word: (fire flag) | (dousing byte) << 16, one v_perm_b32 each
+            // cell m of this word: (fire flag) | (dousing byte) << 16, one v_perm_b32 each; one ds_write_b128
+            uint32_t w[4];
 #pragma unroll
             for (int m = 0; m < 4; ++m)
-                cp[4 * j + m] =
-                    __builtin_amdgcn_perm(sdw[it][j], f, 0x0C000C00u | ((4u + (uint32_t)m) << 16) | (uint32_t)m);
+                w[m] = __builtin_amdgcn_perm(sdw[it][j], f, 0x0C000C00u | ((4u + (uint32_t)m) << 16) | (uint32_t)m);
+            *reinterpret_cast<uint4*>(cp + 4 * ((j + (cq >> 2)) & 3)) = make_uint4(w[0], w[1], w[2], w[3]);
         }
         FB[sr * NCH + cq] = (uint16_t)bits;
         near_fire |= (bits != 0u && sr >= RS - 1 && sr <= RS + TH) ? 1 : 0;
@@ -401,7 +416,8 @@ __global__ __launch_bounds__(256, GCA_ALEX_WGS) void alex_step_kernel(
     // ---- heat and dousing from box sums B_k (fire field) and D_1, D_2 (dousing field):
     //   heat = sum_k n_k*w_k = sum_{k=0..R} B_k * dw_k   (dw_k = w_k - w_{k+1}, w_{R+1} = 0: p.heat_dw)
     //   dous = inner*D_1 + border*(D_2 - D_1) = (inner - border)*D_1 + border*D_2
-    // Fixed evaluation order, every op separately rounded: bit-identical with the C oracle.
+    // Fixed evaluation order: heat accumulates by fma (ph = fma(dw_k, B_k, ph)), dous = fma(border, D_2,
+    // (inner - border) * D_1); bit-identical with the C oracle (fmaf).
     // Pairs of cells share one packed mul / add; B_k <= (2R+1)^2 <= 225 for R <= 7 -> v_cvt_f32_ubyte0.
     f2 ph2[8], dz2[8];
 #pragma unroll
@@ -413,34 +429,65 @@ __global__ __launch_bounds__(256, GCA_ALEX_WGS) void alex_step_kernel(
     auto fire_f = [](uint32_t s) -> float { return R <= 7 ? (float)(s & 0xFFu) : (float)(s & 0xFFFFu); };
     if (wave_need) {
 #ifndef GCA_ABL_NOHEAT
+        // Window sums by lane-local prefix + DPP halo: lane q reads only its own 16 columns of the two
+        // prefix rows (4 + 4 ds_read_b128), V = bottom - top; P = inclusive prefix of V over the 16
+        // columns. The k columns left of the lane are the left lane's suffix T(m) = P(15) - P(15 - m)
+        // (DPP row_shr:1), those right of it the right lane's P(m - 1) (DPP row_shl:1); the 16-lane DPP
+        // row is the image row of the workgroup. Lanes 0 / 15 keep the DPP `old` value: 0 (columns
+        // outside the grid when the tile spans the grid's width) or, when tiles_c > 1, the staged halo
+        // chunk's sums. All sums are exact u32 arithmetic on the packed fire | dousing << 16 columns.
+        const bool halo_lds = tiles_c > 1;  // grid-uniform
+        int goff[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) goff[g] = 16 * (q + 1) + 4 * ((g + ((q + 1) >> 2)) & 3);
 #pragma unroll
         for (int k = 0; k <= RS; ++k) {
-            uint32_t V[16 + 2 * RS];
-            const uint32_t* top = CP + (rr - k) * CWP + 17 * (q + 1);  // = pcol(cc0)
-            const uint32_t* bot = CP + (rr + k + 1) * CWP + 17 * (q + 1);
+            const uint32_t* top = CP + (rr - k) * CWP;
+            const uint32_t* bot = CP + (rr + k + 1) * CWP;
+            uint32_t P[16];
 #pragma unroll
-            for (int j = 0; j < 16 + 2 * RS; ++j) {
-                if (j < 16 + 2 * k) {
-                    const int t = j - k;                                      // column cc0 + t, t in [-k, 16 + k)
-                    const int off = t + (t >= 16 ? 1 : 0) - (t < 0 ? 1 : 0);  // pcol(cc0 + t) - pcol(cc0)
-                    V[j] = bot[off] - top[off];
-                }
-                if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);  // <= 16 LDS reads in flight (VGPR budget)
+            for (int g = 0; g < 4; ++g) {
+                const uint4 b4 = *reinterpret_cast<const uint4*>(bot + goff[g]);
+                const uint4 t4 = *reinterpret_cast<const uint4*>(top + goff[g]);
+                P[4 * g + 0] = b4.x - t4.x;
+                P[4 * g + 1] = b4.y - t4.y;
+                P[4 * g + 2] = b4.z - t4.z;
+                P[4 * g + 3] = b4.w - t4.w;
             }
-            uint32_t s = 0u, sprev = 0u;
 #pragma unroll
-            for (int j = 0; j <= 2 * RS; ++j)
-                if (j <= 2 * k) s += V[j];
+            for (int i = 1; i < 16; ++i) P[i] += P[i - 1];
+            uint32_t Lh[RS + 1], Rh[RS + 1];  // Lh[m]: sum of the m columns left of the lane, Rh[m]: right
+#pragma unroll
+            for (int m = 1; m <= k; ++m) {
+                Lh[m] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(P[15] - P[15 - m]), 0x111, 0xF, 0xF, false);
+                Rh[m] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)P[m - 1], 0x101, 0xF, 0xF, false);
+            }
+            if (halo_lds && k > 0) {  // lanes 0 / 15: the staged chunks left / right of the tile
+                uint32_t al = 0u, ar = 0u;
+#pragma unroll
+                for (int m = 1; m <= k; ++m) {
+                    const int cl = pcol(16 * q + 16 - m), cr = pcol(16 * (q + 2) + m - 1);
+                    al += bot[cl] - top[cl];
+                    ar += bot[cr] - top[cr];
+                    Lh[m] = q == 0 ? al : Lh[m];
+                    Rh[m] = q == 15 ? ar : Rh[m];
+                }
+            }
             const float wk = k <= R ? p.heat_dw[k] : 0.0f;
+            uint32_t sprev = 0u;
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
-                if (i > 0) s += V[i + 2 * k] - V[i - 1];
+                const int hi = i + k < 15 ? i + k : 15, lo = i - k - 1;
+                uint32_t s = P[hi];
+                if (lo >= 0) s -= P[lo];
+                if (i < k) s += Lh[k - i];
+                if (i + k > 15) s += Rh[i + k - 15];
                 if (i & 1) {
                     const int j = i >> 1;
-                    if (k <= R) ph2[j] = ph2[j] + (f2){wk, wk} * (f2){fire_f(sprev), fire_f(s)};
+                    if (k <= R) ph2[j] = __builtin_elementwise_fma((f2){wk, wk}, (f2){fire_f(sprev), fire_f(s)}, ph2[j]);
                     const f2 dsum = {(float)(sprev >> 16), (float)(s >> 16)};
                     if (k == 1) dz2[j] = (f2){w_in_minus_bd, w_in_minus_bd} * dsum;
-                    if (k == 2) dz2[j] = dz2[j] + (f2){p.dous_border, p.dous_border} * dsum;
+                    if (k == 2) dz2[j] = __builtin_elementwise_fma((f2){p.dous_border, p.dous_border}, dsum, dz2[j]);
                 }
                 sprev = s;
             }

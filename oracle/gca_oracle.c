@@ -9,8 +9,8 @@
  *
  * Restated algorithm, per cell (r, c) of env e, zero (EMPTY) padding:
  *   B_k   = #FIRE in the (2k+1)^2 box, D_k = sum of dousing in the box (k = 1, 2)
- *   heat  = sum_{k=0..R} dw_k * B_k         (dw_k = w_k - w_{k+1}: ring weights, f32)
- *   dous  = (inner - border) * D_1 + border * D_2
+ *   heat  = sum_{k=0..R} dw_k * B_k         (dw_k = w_k - w_{k+1}: ring weights, f32; ph = fmaf(dw_k, B_k, ph))
+ *   dous  = (inner - border) * D_1 + border * D_2   (the second term by fmaf)
  *   p_h   = heat - dous                      (:198)
  *   p_d   = ((((p_h * av) * ad) * wind[d]) * p_slope[d])                       (:206)
  *   injected: TREE -> FIRE iff exists fire neighbour d with u[d] < p_d (:379-383)
@@ -159,9 +159,9 @@ static void alex_env(const oracle_alex_params* p, int e, int H, int W, const uin
                 const long W1 = W + 1;
                 const int64_t fire_n = satf[r1 * W1 + c1] - satf[r0 * W1 + c1] - satf[r1 * W1 + c0] + satf[r0 * W1 + c0];
                 const int64_t dsum = satd[r1 * W1 + c1] - satd[r0 * W1 + c1] - satd[r1 * W1 + c0] + satd[r0 * W1 + c0];
-                if (k <= R) ph = ph + p->heat_dw[k] * (float)fire_n;
+                if (k <= R) ph = fmaf(p->heat_dw[k], (float)fire_n, ph);
                 if (k == 1) dz = in_minus_bd * (float)dsum;
-                if (k == 2) dz = dz + p->dous_border * (float)dsum;
+                if (k == 2) dz = fmaf(p->dous_border, (float)dsum, dz);
             }
             ph = ph - dz;
             /* neighbourhood fire mask, d = (a,b) row-major without the centre */
