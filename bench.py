@@ -28,9 +28,10 @@ for _p in (ROOT, os.path.join(ROOT, "gym-cellular-automata_amd")):
         sys.path.insert(0, _p)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-# algorithmic HBM bytes per Alexandridis cell-update: grid r+w 2, age r+w 4, veg 1, den 1,
-# dousing 1, + slopes: edge layout 4 x f32 = 16 (gca_alex_step_es), 8-plane p_slope 8 x f32 = 32
-ALEX_BYTES = {"edge": 25, "planes": 41}
+# HBM bytes per Alexandridis cell-update this build moves: grid r+w 2, age r+w 4, veg 1, den 1,
+# dousing 1, + slopes: edge layout 4 x f32 = 16 (gca_alex_step_es), 8-plane p_slope 8 x f32 = 32;
+# packed env layout (gca_alex_step_packed): veg|den in one byte, dousing 1 bit, edge slopes 16
+ALEX_BYTES = {"packed": 23.125, "edge": 25, "planes": 41}
 ALEX_BYTES_PER_CELL = 41  # the SURVEY.md §8d figure (8-plane layout), reported alongside
 WINDY_BYTES_PER_CELL = 2  # u8 read + u8 write
 
@@ -46,7 +47,7 @@ def parse():
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--slope-layout", choices=["edge", "planes"], default="edge")
+    ap.add_argument("--slope-layout", choices=["packed", "edge", "planes"], default="packed")
     ap.add_argument("--headline-only", action="store_true",
                     help="only the headline loop (no RGB / episode-start loops): every alex_step launch is the "
                          "dense mid-episode one, so rocprofv3 per-kernel averages match kernel_ms")
@@ -143,9 +144,7 @@ def bench_alex(args, world, rank, device, pg):
             events.append((a, b))
         else:
             env.ca_step()
-        call("gca_advenv_post", env.env_params, dev.ptr(action), dev.ptr(env.pos), dev.ptr(env.accu),
-             dev.ptr(env.wind_index), dev.ptr(env.time_step), dev.ptr(env.is_night), dev.ptr(env.dousing), N, N,
-             dev.ptr(env.counts), dev.ptr(env.rng_step), dev.ptr(env.reward), dev.ptr(env.done), E, st)
+        env.post_step(action)
         if gathered is not None and args.gather == "step":
             # RCCL all-gather of the per-env done mask + reward
             payload = torch.cat([env.done, env.reward.view(torch.uint8)])
@@ -230,9 +229,7 @@ def bench_config4(args, world, rank, device, pg):
             events.append((a, b))
         else:
             env.ca_step()
-        call("gca_advenv_post", env.env_params, dev.ptr(action), dev.ptr(env.pos), dev.ptr(env.accu),
-             dev.ptr(env.wind_index), dev.ptr(env.time_step), dev.ptr(env.is_night), dev.ptr(env.dousing), N, N,
-             dev.ptr(env.counts), dev.ptr(env.rng_step), dev.ptr(env.reward), dev.ptr(env.done), E, st)
+        env.post_step(action)
 
     dt, kern = timed_loop(step, args.steps, args.warmup, pg, device)
     out = {"config": "AdvancedBulldozer 256x256, hidden foliage/altitude layers (use_hidden=True), 4096 envs/GPU",
@@ -463,7 +460,8 @@ def measured_traffic(args):
         data = json.load(open(tf))
     except (ValueError, OSError):
         return None
-    want = "alex_step<6, 0, true, %s>" % ("true" if args.slope_layout == "edge" else "false")
+    want = {"packed": "alex_step<6, 0, true, true, true>", "edge": "alex_step<6, 0, true, true, false>",
+            "planes": "alex_step<6, 0, true, false, false>"}[args.slope_layout]
     for k, v in data.items():  # the Philox-mode FAST kernel at R = 6 (N = 256) of this slope layout
         if k == want:
             return v.get("bytes_per_launch")
@@ -537,7 +535,7 @@ def main():
             # (edge-slope layout: 25 B/cell) and the PMC traffic are reported beside it
             "roofline": {"bound": "hbm", "achieved": alex["survey_equiv_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": alex["survey_equiv_gbs"] / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "alex_step_kernel" + ("<ES>" if args.slope_layout == "edge" else ""),
+                         "kernel": "alex_step_kernel" + {"packed": "<ES, PK>", "edge": "<ES>", "planes": ""}[args.slope_layout],
                          "kernel_ms": alex["kernel_ms"],
                          "algorithmic_bytes_per_cell": ALEX_BYTES_PER_CELL,
                          "slope_layout": args.slope_layout,

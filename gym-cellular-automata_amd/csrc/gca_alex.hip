@@ -128,10 +128,16 @@ template <class T, class S> __device__ __forceinline__ T bitcast_(S s) {
 // only matter for TREE cells with a burning neighbour. A workgroup with no FIRE within one cell of its tile
 // skips the heat phase; a wave with no such TREE cell skips the direction pass and its loads (a real
 // episode's fire front covers a few tiles of 256). Results are unchanged (the skipped values are unused).
+//
+// PK (packed env layout, ES + FAST + Philox mode only: gca_alex_step_packed): `veg` holds vd = min(veg, 7) |
+// min(den, 7) << 4 (one byte per cell), `dousing` one bit per cell (a u16 per 16-column chunk, bit i = column
+// 16j + i; the env's dousing counts are 0/1) and the edge slopes are stored coalesced: inside every 256-column
+// row segment of a plane, column 16q + 4m + j sits at position 64m + 4q + j, so the 16 lanes of an image row
+// read 256 contiguous bytes per load instruction. 23.125 B of HBM traffic per cell instead of 25.
 #ifndef GCA_ALEX_WGS
 #define GCA_ALEX_WGS 4
 #endif
-template <int R, int MODE, bool FAST, bool ES>
+template <int R, int MODE, bool FAST, bool ES, bool PK = false>
 __global__ __launch_bounds__(256, GCA_ALEX_WGS) void alex_step_kernel(
     gca_alex_params p, int H, int W, int tiles_r, int tiles_c, const uint8_t* __restrict__ grid_in,
     uint8_t* __restrict__ grid_out, const int16_t* __restrict__ age_in, int16_t* __restrict__ age_out,
@@ -164,6 +170,8 @@ __global__ __launch_bounds__(256, GCA_ALEX_WGS) void alex_step_kernel(
     const int64_t HW = (int64_t)H * W;
     const uint8_t* gE = grid_in + (int64_t)e * HW;
     const uint8_t* dE = dousing + (int64_t)e * HW;
+    const uint16_t* dbE = reinterpret_cast<const uint16_t*>(dousing) + (int64_t)e * (HW >> 4);  // PK: dousing bits
+    static_assert(!PK || (ES && FAST && MODE == 0), "packed layout: edge slopes, FAST shape, Philox mode");
     const int tid = threadIdx.x;
     const bool rows16 = FAST || (((W & 15) == 0) &&
                                  ((((uintptr_t)grid_in) | ((uintptr_t)dousing) | ((uintptr_t)grid_out) |
@@ -207,7 +215,12 @@ __global__ __launch_bounds__(256, GCA_ALEX_WGS) void alex_step_kernel(
         }
     }
     auto load_vd = [&]() {
-        if (vec) {
+        if (PK) {  // vd = veg | den << 4 (both already min(., 7))
+            const uint4 v4 = *reinterpret_cast<const uint4*>(vE + lo);
+            vgw[0] = v4.x & 0x0F0F0F0Fu; vgw[1] = v4.y & 0x0F0F0F0Fu; vgw[2] = v4.z & 0x0F0F0F0Fu; vgw[3] = v4.w & 0x0F0F0F0Fu;
+            dnw[0] = (v4.x >> 4) & 0x0F0F0F0Fu; dnw[1] = (v4.y >> 4) & 0x0F0F0F0Fu;
+            dnw[2] = (v4.z >> 4) & 0x0F0F0F0Fu; dnw[3] = (v4.w >> 4) & 0x0F0F0F0Fu;
+        } else if (vec) {
             const uint4 v4 = *reinterpret_cast<const uint4*>(vE + lo);
             const uint4 d4 = *reinterpret_cast<const uint4*>(nE + lo);
             vgw[0] = v4.x; vgw[1] = v4.y; vgw[2] = v4.z; vgw[3] = v4.w;
@@ -241,8 +254,9 @@ __global__ __launch_bounds__(256, GCA_ALEX_WGS) void alex_step_kernel(
         const int dr = (ES && k >= 4 && r + 1 < H) ? 1 : 0;
         const float* src = psE + (uint32_t)(plane * (uint32_t)HW) + lo + (uint32_t)(dr * W);
         if (vec) {
+            // PK: coalesced segment order, lane q's columns 16q + 4m .. +3 at segment position 64m + 4q
 #pragma unroll
-            for (int m = 0; m < 4; ++m) v[m] = *reinterpret_cast<const float4*>(src + 4 * m);
+            for (int m = 0; m < 4; ++m) v[m] = *reinterpret_cast<const float4*>(src + (PK ? 64 * m - 12 * q : 4 * m));
         } else {
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
@@ -289,9 +303,15 @@ __global__ __launch_bounds__(256, GCA_ALEX_WGS) void alex_step_kernel(
         if (ch < RR * NCH && gr >= 0 && gr < H) {
             if (rows16 && gc >= 0 && gc + 16 <= W) {  // FAST: a chunk is entirely inside or outside
                 const uint4 a = *reinterpret_cast<const uint4*>(gE + (int64_t)gr * W + gc);
-                const uint4 b = *reinterpret_cast<const uint4*>(dE + (int64_t)gr * W + gc);
                 gw[0] = a.x; gw[1] = a.y; gw[2] = a.z; gw[3] = a.w;
-                dw[0] = b.x; dw[1] = b.y; dw[2] = b.z; dw[3] = b.w;
+                if (PK) {  // 16 dousing bits -> 0x01 bytes
+                    const uint32_t b16 = dbE[((uint32_t)gr * (uint32_t)W + (uint32_t)gc) >> 4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) dw[j] = spread4(b16 >> (4 * j));
+                } else {
+                    const uint4 b = *reinterpret_cast<const uint4*>(dE + (int64_t)gr * W + gc);
+                    dw[0] = b.x; dw[1] = b.y; dw[2] = b.z; dw[3] = b.w;
+                }
             } else if (!FAST) {
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
@@ -795,7 +815,7 @@ __global__ void alex_prepare_slope_kernel(const float* __restrict__ slope, float
     }
 }
 
-template <int R, int MODE, bool ES>
+template <int R, int MODE, bool ES, bool PK = false>
 void launch_alex(const gca_alex_params& p, int E, int H, int W, const uint8_t* gi, uint8_t* go, const int16_t* ai,
                  int16_t* ao, const uint8_t* veg, const uint8_t* den, const uint8_t* dous, const float* ps,
                  const int32_t* wi, const uint32_t* rs, const float* ib, const float* ig, const int32_t* ia, float* po,
@@ -808,7 +828,10 @@ void launch_alex(const gca_alex_params& p, int E, int H, int W, const uint8_t* g
     const bool fast = MODE == 0 && W % TW == 0 && H % TH == 0 &&
                       ((((uintptr_t)gi) | ((uintptr_t)go) | ((uintptr_t)ai) | ((uintptr_t)ao) | ((uintptr_t)veg) |
                         ((uintptr_t)den) | ((uintptr_t)dous) | ((uintptr_t)ps)) & 15u) == 0;
-    if (fast)  // production shape: no per-lane bounds checks (instantiated for the Philox mode only)
+    if (PK)  // packed env layout (the host checked the FAST shape and alignment)
+        hipLaunchKernelGGL((alex_step_kernel<R, 0, true, true, true>), grid, dim3(256), lds, st, p, H, W, tiles_r,
+                           tiles_c, gi, go, ai, ao, veg, den, dous, ps, wi, rs, ib, ig, ia, po, counts);
+    else if (fast)  // production shape: no per-lane bounds checks (instantiated for the Philox mode only)
         hipLaunchKernelGGL((alex_step_kernel<R, MODE, MODE == 0, ES>), grid, dim3(256), lds, st, p, H, W, tiles_r,
                            tiles_c, gi, go, ai, ao, veg, den, dous, ps, wi, rs, ib, ig, ia, po, counts);
     else
@@ -816,13 +839,13 @@ void launch_alex(const gca_alex_params& p, int E, int H, int W, const uint8_t* g
                            gi, go, ai, ao, veg, den, dous, ps, wi, rs, ib, ig, ia, po, counts);
 }
 
-template <int MODE, bool ES>
+template <int MODE, bool ES, bool PK = false>
 void dispatch_r(int R, const gca_alex_params& p, int E, int H, int W, const uint8_t* gi, uint8_t* go, const int16_t* ai,
                 int16_t* ao, const uint8_t* veg, const uint8_t* den, const uint8_t* dous, const float* ps,
                 const int32_t* wi, const uint32_t* rs, const float* ib, const float* ig, const int32_t* ia, float* po,
                 int32_t* counts, hipStream_t st) {
 #define GCA_ALEX_CASE(RV) \
-    case RV: launch_alex<RV, MODE, ES>(p, E, H, W, gi, go, ai, ao, veg, den, dous, ps, wi, rs, ib, ig, ia, po, counts, st); break;
+    case RV: launch_alex<RV, MODE, ES, PK>(p, E, H, W, gi, go, ai, ao, veg, den, dous, ps, wi, rs, ib, ig, ia, po, counts, st); break;
     switch (R) {
         GCA_ALEX_CASE(1) GCA_ALEX_CASE(2) GCA_ALEX_CASE(3) GCA_ALEX_CASE(4)
         GCA_ALEX_CASE(5) GCA_ALEX_CASE(6) GCA_ALEX_CASE(7) GCA_ALEX_CASE(8)
@@ -890,6 +913,83 @@ extern "C" int gca_alex_step_es(const gca_alex_params* p, int E, int H, int W, c
                                 void* stream) {
     return alex_step_impl(true, p, E, H, W, grid_in, grid_out, age_in, age_out, veg, den, dousing, edge_slope,
                           wind_index, rng_step, inj_burn, inj_grow, inj_age, prob_out, counts, stream);
+}
+
+extern "C" int gca_alex_step_packed(const gca_alex_params* p, int E, int H, int W, const uint8_t* grid_in,
+                                    uint8_t* grid_out, const int16_t* age_in, int16_t* age_out, const uint8_t* vd,
+                                    const uint16_t* dous_bits, const float* edge_slope_coal, const int32_t* wind_index,
+                                    const uint32_t* rng_step, int32_t* counts, void* stream) {
+    GCA_CHECK_ARG(p && grid_in && grid_out && age_in && age_out && vd && dous_bits && edge_slope_coal && wind_index,
+                  "alex_step_packed: null argument");
+    GCA_CHECK_ARG(E > 0 && H > 0 && W > 0 && W % TW == 0 && H % TH == 0,
+                  "alex_step_packed: W must be a multiple of 256 and H of 16");
+    GCA_CHECK_ARG(p->R >= 1 && p->R <= GCA_MAX_RADIUS, "alex_step_packed: burn radius must be in [1, 8]");
+    GCA_CHECK_ARG(p->n_winds >= 1 && p->n_winds <= 16, "alex_step_packed: 1..16 wind matrices");
+    GCA_CHECK_ARG(grid_in != grid_out && age_in != age_out, "alex_step_packed: in-place update is not supported");
+    GCA_CHECK_ARG(((((uintptr_t)grid_in) | ((uintptr_t)grid_out) | ((uintptr_t)age_in) | ((uintptr_t)age_out) |
+                    ((uintptr_t)vd) | ((uintptr_t)edge_slope_coal)) & 15u) == 0 && ((uintptr_t)dous_bits & 1u) == 0,
+                  "alex_step_packed: arrays must be 16-B aligned");
+    hipStream_t st = (hipStream_t)stream;
+    if (counts && hipMemsetAsync(counts, 0, sizeof(int32_t) * 3 * (size_t)E, st) != hipSuccess) {
+        gca_set_error("alex_step_packed: counts memset failed");
+        return GCA_ERR_HIP;
+    }
+    dispatch_r<0, true, true>(p->R, *p, E, H, W, grid_in, grid_out, age_in, age_out, vd, nullptr,
+                              reinterpret_cast<const uint8_t*>(dous_bits), edge_slope_coal, wind_index, rng_step, nullptr,
+                              nullptr, nullptr, nullptr, counts, st);
+    GCA_CHECK_LAUNCH("alex_step_packed");
+    return GCA_OK;
+}
+
+// ------------------------------------------------------------------ packed env layers
+namespace {
+// one thread per 16-cell chunk: vd = min(veg, 7) | min(den, 7) << 4, dousing bit = (count != 0)
+__global__ void alex_pack_layers_kernel(const uint8_t* __restrict__ veg, const uint8_t* __restrict__ den,
+                                        const uint8_t* __restrict__ dous, uint8_t* __restrict__ vd,
+                                        uint16_t* __restrict__ dbits, int64_t nchunks) {
+    const int64_t ch = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (ch >= nchunks) return;
+    uint16_t b = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int64_t c = ch * 16 + i;
+        if (vd) vd[c] = (uint8_t)(min((int)veg[c], 7) | (min((int)den[c], 7) << 4));
+        b |= (uint16_t)((dous[c] != 0 ? 1u : 0u) << i);
+    }
+    dbits[ch] = b;
+}
+// coalesced edge-slope order: inside every 256-column segment, column 16q + 4m + j -> position 64m + 4q + j
+__global__ void alex_edge_coalesce_kernel(const float* __restrict__ in, float* __restrict__ out, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t seg = i >> 8;
+    const int c = (int)(i & 255), q = c >> 4, m = (c >> 2) & 3, j = c & 3;
+    out[(seg << 8) + 64 * m + 4 * q + j] = in[i];
+}
+}  // namespace
+
+extern "C" int gca_alex_pack_layers(const uint8_t* veg, const uint8_t* den, const uint8_t* dousing, uint8_t* vd,
+                                    uint16_t* dous_bits, int E, int H, int W, void* stream) {
+    GCA_CHECK_ARG(dousing && dous_bits && E > 0 && H > 0 && W > 0 && W % 16 == 0,
+                  "pack_layers: dousing, dous_bits and W % 16 == 0 required");
+    GCA_CHECK_ARG(!vd || (veg && den), "pack_layers: vd needs veg and den");
+    const int64_t nch = (int64_t)E * H * W / 16;
+    hipLaunchKernelGGL(alex_pack_layers_kernel, dim3((unsigned)((nch + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       veg, den, dousing, vd, dous_bits, nch);
+    GCA_CHECK_LAUNCH("pack_layers");
+    return GCA_OK;
+}
+
+extern "C" int gca_alex_edge_slope_coalesce(const float* edge_slope, float* edge_slope_coal, int E, int H, int W,
+                                            void* stream) {
+    GCA_CHECK_ARG(edge_slope && edge_slope_coal && edge_slope != edge_slope_coal && E > 0 && H > 0 && W > 0 &&
+                      W % TW == 0,
+                  "edge_slope_coalesce: distinct arrays and W % 256 == 0 required");
+    const int64_t n = (int64_t)E * 4 * H * W;
+    hipLaunchKernelGGL(alex_edge_coalesce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       edge_slope, edge_slope_coal, n);
+    GCA_CHECK_LAUNCH("edge_slope_coalesce");
+    return GCA_OK;
 }
 
 // ------------------------------------------------------------------ slope from altitude

@@ -155,7 +155,8 @@ extern "C" int gca_bulldozer_post(const gca_bulldozer_params* p, int last_pass, 
 __global__ void advenv_post_kernel(gca_advenv_params p, const int32_t* __restrict__ action, int32_t* __restrict__ pos,
                                    float* __restrict__ accu, int32_t* __restrict__ wind_index,
                                    int32_t* __restrict__ time_step, int32_t* __restrict__ is_night,
-                                   uint8_t* __restrict__ dousing, int H, int W, const int32_t* __restrict__ counts,
+                                   uint8_t* __restrict__ dousing, uint16_t* __restrict__ dous_bits, int H, int W,
+                                   const int32_t* __restrict__ counts,
                                    uint32_t* __restrict__ rng_step, float* __restrict__ reward,
                                    uint8_t* __restrict__ done, int E) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -175,7 +176,11 @@ __global__ void advenv_post_kernel(gca_advenv_params p, const int32_t* __restric
     move_pos(a0, row, col, H, W, p.up_mask, p.down_mask, p.left_mask, p.right_mask);
     pos[2 * e] = row;
     pos[2 * e + 1] = col;
-    if (a1 == 1) dousing[(int64_t)e * H * W + (int64_t)row * W + col] = 1;
+    if (a1 == 1) {
+        const int64_t cell = (int64_t)e * H * W + (int64_t)row * W + col;
+        dousing[cell] = 1;
+        if (dous_bits) dous_bits[cell >> 4] |= (uint16_t)(1u << (cell & 15));  // packed layout (one writer per env)
+    }
     // time_step / is_night (advanced_bulldozer.py:1118,1123-1127)
     const int ts = time_step[e] + 1;
     time_step[e] = ts;
@@ -189,15 +194,16 @@ __global__ void advenv_post_kernel(gca_advenv_params p, const int32_t* __restric
 }
 
 extern "C" int gca_advenv_post(const gca_advenv_params* p, const int32_t* action, int32_t* pos, float* accu,
-                               int32_t* wind_index, int32_t* time_step, int32_t* is_night, uint8_t* dousing, int H,
-                               int W, const int32_t* counts, uint32_t* rng_step, float* reward, uint8_t* done, int E,
-                               void* stream) {
+                               int32_t* wind_index, int32_t* time_step, int32_t* is_night, uint8_t* dousing,
+                               uint16_t* dous_bits, int H, int W, const int32_t* counts, uint32_t* rng_step,
+                               float* reward, uint8_t* done, int E, void* stream) {
     GCA_CHECK_ARG(p && action && pos && accu && wind_index && time_step && is_night && dousing && counts && rng_step &&
                       reward && done && E > 0,
                   "advenv_post: null argument");
     GCA_CHECK_ARG(p->n_winds > 0, "advenv_post: n_winds > 0");
+    GCA_CHECK_ARG(!dous_bits || (W % 16 == 0), "advenv_post: dousing bits need W % 16 == 0");
     hipLaunchKernelGGL(advenv_post_kernel, ENV_GRID(E), 0, (hipStream_t)stream, *p, action, pos, accu, wind_index,
-                       time_step, is_night, dousing, H, W, counts, rng_step, reward, done, E);
+                       time_step, is_night, dousing, dous_bits, H, W, counts, rng_step, reward, done, E);
     GCA_CHECK_LAUNCH("advenv_post");
     return GCA_OK;
 }
@@ -207,7 +213,8 @@ extern "C" int gca_advenv_post(const gca_advenv_params* p, const int32_t* action
 __global__ __launch_bounds__(256) void reset_cells_kernel(const uint8_t* __restrict__ done, int64_t HW, int cpe,
                                                           uint8_t* __restrict__ grid, const uint8_t* __restrict__ grid0,
                                                           int16_t* __restrict__ age, const int16_t* __restrict__ age0,
-                                                          uint8_t* __restrict__ dous, const uint8_t* __restrict__ dous0) {
+                                                          uint8_t* __restrict__ dous, const uint8_t* __restrict__ dous0,
+                                                          uint16_t* __restrict__ dbits) {
     const int e = blockIdx.x / cpe;
     if (!done[e]) return;
     const int64_t base = (int64_t)e * HW;
@@ -217,6 +224,8 @@ __global__ __launch_bounds__(256) void reset_cells_kernel(const uint8_t* __restr
         if (age) age[base + i] = age0[base + i];
         if (dous) dous[base + i] = dous0 ? dous0[base + i] : 0;
     }
+    if (dbits)  // packed dousing bits of this chunk (zeroed: the reset state has no dousing)
+        for (int64_t i = begin / 16 + threadIdx.x; i < end / 16; i += 256) dbits[(base >> 4) + i] = 0;
 }
 
 __global__ void reset_env_kernel(uint8_t* __restrict__ done, int32_t* __restrict__ pos,
@@ -235,19 +244,20 @@ __global__ void reset_env_kernel(uint8_t* __restrict__ done, int32_t* __restrict
 
 extern "C" int gca_reset_where(const uint8_t* done, int E, int H, int W, uint8_t* grid, const uint8_t* grid0,
                                int16_t* age, const int16_t* age0, uint8_t* dousing, const uint8_t* dousing0,
-                               int32_t* pos, const int32_t* pos0, float* accu, int32_t* wind_index,
+                               uint16_t* dous_bits, int32_t* pos, const int32_t* pos0, float* accu, int32_t* wind_index,
                                const int32_t* wind_index0, void* stream) {
     GCA_CHECK_ARG(done && E > 0 && H > 0 && W > 0, "reset_where: done and sizes required");
     GCA_CHECK_ARG(!grid || grid0, "reset_where: grid needs grid0");
     GCA_CHECK_ARG(!age || age0, "reset_where: age needs age0");
     GCA_CHECK_ARG(!pos || pos0, "reset_where: pos needs pos0");
     GCA_CHECK_ARG(!wind_index || wind_index0, "reset_where: wind_index needs wind_index0");
+    GCA_CHECK_ARG(!dous_bits || (!dousing0 && W % 16 == 0), "reset_where: dousing bits are zeroed (no dousing0), W % 16 == 0");
     hipStream_t st = (hipStream_t)stream;
     const int64_t HW = (int64_t)H * W;
     const int cpe = (int)((HW + 4095) / 4096);
-    if (grid || age || dousing) {
+    if (grid || age || dousing || dous_bits) {
         hipLaunchKernelGGL(reset_cells_kernel, dim3((unsigned)((int64_t)E * cpe)), dim3(256), 0, st, done, HW, cpe, grid,
-                           grid0, age, age0, dousing, dousing0);
+                           grid0, age, age0, dousing, dousing0, dous_bits);
         GCA_CHECK_LAUNCH("reset_cells");
     }
     hipLaunchKernelGGL(reset_env_kernel, ENV_GRID(E), 0, st, (uint8_t*)done, pos, pos0, accu, wind_index, wind_index0, E);

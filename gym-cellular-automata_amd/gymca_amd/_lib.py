@@ -137,12 +137,15 @@ _SIGNATURES = {
     "gca_alex_step_es": ([POINTER(AlexParams), c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
                          c_int),
     "gca_alex_edge_slope_from_altitude": ([P, P, c_int, c_int, c_int, P], c_int),
+    "gca_alex_step_packed": ([POINTER(AlexParams), c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, P], c_int),
+    "gca_alex_pack_layers": ([P, P, P, P, P, c_int, c_int, c_int, P], c_int),
+    "gca_alex_edge_slope_coalesce": ([P, P, c_int, c_int, c_int, P], c_int),
     "gca_alex_edge_factors": ([P, P, P, c_int64, P], c_int),
     "gca_adv_observation": ([POINTER(ObsParams), c_int, c_int, c_int, c_int, P, P, P, P, P, P, c_int, P, P, P],
                             c_int),
     "gca_alex_altitude_apply": ([P, c_int, c_int, c_int, P, P, P, P, P], c_int),
-    "gca_advenv_post": ([POINTER(AdvEnvParams), P, P, P, P, P, P, P, c_int, c_int, P, P, P, P, c_int, P], c_int),
-    "gca_reset_where": ([P, c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, P, P], c_int),
+    "gca_advenv_post": ([POINTER(AdvEnvParams), P, P, P, P, P, P, P, P, c_int, c_int, P, P, P, P, c_int, P], c_int),
+    "gca_reset_where": ([P, c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, P, P, P], c_int),
     "gca_fill_categorical": ([P, c_int64, c_int, c_int, c_uint64, P, P, c_int, P], c_int),
     "gca_random_actions": ([P, c_int, c_int, c_uint64, P, P], c_int),
     "gca_ds_count_draws": ([P, c_int, c_int, c_int, c_int, c_int, c_int, P, P], c_int),

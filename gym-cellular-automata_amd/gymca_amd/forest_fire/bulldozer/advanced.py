@@ -18,8 +18,11 @@ Device layout per env: grid u8 (ping-pong), fire_age i16 (ping-pong), vegetation
 density / dousing u8, the slopes in the antisymmetric edge layout f32 [4][H][W]
 (0.078 * slope toward the 4 preceding neighbours, built once from altitude; the step
 derives the other 4 directions and exp in-kernel: gca_alex_step_es), plus per-env
-scalars: 25 B of HBM traffic per cell-update. slope_layout="planes" keeps
-the general 8-plane p_slope f32 [8][H][W] = exp(0.078*slope) (41 B per cell-update).
+scalars: 25 B of HBM traffic per cell-update. slope_layout="packed" (the default
+"auto" when W % 256 == 0 and H % 16 == 0) runs gca_alex_step_packed on the same state with
+vegetation|density in one byte, the 0/1 dousing counts as bits and the edge slopes in coalesced
+segment order (23.1 B per cell-update; the u8 layers stay the API's context). slope_layout="planes"
+keeps the general 8-plane p_slope f32 [8][H][W] = exp(0.078*slope) (41 B per cell-update).
 """
 import numpy as np
 
@@ -35,7 +38,7 @@ class AdvancedForestFireBulldozerEnv:
     def __init__(self, nrows, ncols, key=0, num_envs=8, speed_move=0.12, speed_act=0.03, speed_multiplier=1.0,
                  pos_bull=None, pos_fire=None, t_move=None, t_shoot=None, t_any=0.001, p_tree=0.90, p_empty=0.10,
                  use_hidden=True, middle_fire=False, enable_extensions=False, device=None, env_offset=0,
-                 hidden_rng=None, slope_layout="edge", observation="grid"):
+                 hidden_rng=None, slope_layout="auto", observation="grid"):
         import torch
 
         self.device = dev.require_device(device)
@@ -80,11 +83,19 @@ class AdvancedForestFireBulldozerEnv:
         self.vegetation = torch.full((E, H, W), 3, dtype=torch.uint8, **kw)
         self.density = torch.full((E, H, W), 3, dtype=torch.uint8, **kw)
         self.dousing = torch.zeros((E, H, W), dtype=torch.uint8, **kw)
-        if slope_layout not in ("edge", "planes"):
-            raise ValueError("slope_layout must be 'edge' or 'planes'")
+        if slope_layout == "auto":
+            slope_layout = "packed" if (W % 256 == 0 and H % 16 == 0) else "edge"
+        if slope_layout not in ("edge", "planes", "packed"):
+            raise ValueError("slope_layout must be 'auto', 'edge', 'packed' or 'planes'")
+        if slope_layout == "packed" and (W % 256 or H % 16):
+            raise ValueError("slope_layout='packed' needs W % 256 == 0 and H % 16 == 0")
         self.slope_layout = slope_layout
-        # edge: (E, 4, H, W) exponents for gca_alex_step_es; planes: (E, 8, H, W) p_slope for gca_alex_step
-        self.slope_data = torch.zeros((E, 4 if slope_layout == "edge" else 8, H, W), dtype=torch.float32, **kw)
+        # edge: (E, 4, H, W) edge values for gca_alex_step_es (packed: the same in coalesced order);
+        # planes: (E, 8, H, W) p_slope for gca_alex_step
+        self.slope_data = torch.zeros((E, 8 if slope_layout == "planes" else 4, H, W), dtype=torch.float32, **kw)
+        # packed layout extras: vd = min(veg, 7) | min(den, 7) << 4 and the dousing bits (u16 per 16 columns)
+        self.vd = torch.zeros((E, H, W), dtype=torch.uint8, **kw) if slope_layout == "packed" else None
+        self.dous_bits = torch.zeros((E, H * W // 16), dtype=torch.int16, **kw) if slope_layout == "packed" else None
         self.wind_index = torch.zeros(E, dtype=torch.int32, **kw)
         self.pos = torch.zeros((E, 2), dtype=torch.int32, **kw)
         self.accu = torch.zeros(E, dtype=torch.float32, **kw)
@@ -128,12 +139,28 @@ class AdvancedForestFireBulldozerEnv:
             self.density.fill_(3)
             self.vegetation.fill_(3)
         self._slopes_from(self.altitude)
+        self._pack_layers()
+
+    def _pack_layers(self):
+        """vd and dousing bits of the packed layout from the u8 layers (no-op for the other layouts)."""
+        if self.vd is None:
+            return
+        E, H, W = self.num_envs, self.nrows, self.ncols
+        call("gca_alex_pack_layers", dev.ptr(self.vegetation), dev.ptr(self.density), dev.ptr(self.dousing),
+             dev.ptr(self.vd), dev.ptr(self.dous_bits), E, H, W, dev.stream_ptr(self.device))
 
     def _slopes_from(self, altitude):
         E, H, W = self.num_envs, self.nrows, self.ncols
         st = dev.stream_ptr(self.device)
         if self.slope_layout == "edge":
             call("gca_alex_edge_slope_from_altitude", dev.ptr(altitude), dev.ptr(self.slope_data), E, H, W, st)
+        elif self.slope_layout == "packed":
+            import torch
+
+            tmp = torch.empty_like(self.slope_data)
+            call("gca_alex_edge_slope_from_altitude", dev.ptr(altitude), dev.ptr(tmp), E, H, W, st)
+            call("gca_alex_edge_slope_coalesce", dev.ptr(tmp), dev.ptr(self.slope_data), E, H, W, st)
+            del tmp
         else:
             call("gca_alex_slope_from_altitude", dev.ptr(altitude), dev.ptr(self.slope_data), None, E, H, W, st)
 
@@ -180,6 +207,8 @@ class AdvancedForestFireBulldozerEnv:
         wi = rng.integers(0, 8, size=E) if self.use_hidden else np.zeros(E)
         self.wind_index.copy_(torch.as_tensor(wi.astype(np.int32), device=self.device))
         self.dousing.zero_()
+        if self.dous_bits is not None:
+            self.dous_bits.zero_()
         self.accu.zero_()
         self.time_step.fill_(1)
         self.is_night.zero_()
@@ -220,6 +249,9 @@ class AdvancedForestFireBulldozerEnv:
             put(self.wind_index, wind_index, torch.int32)
         if dousing is not None:
             put(self.dousing, dousing, torch.uint8)
+            if self.dous_bits is not None and bool((self.dousing > 1).any()):
+                raise ValueError("the packed layout stores dousing counts as bits: values must be 0/1 "
+                                 "(use slope_layout='edge' for other counts)")
         if position is not None:
             put(self.pos, position, torch.int32)
         if altitude is not None:
@@ -227,6 +259,8 @@ class AdvancedForestFireBulldozerEnv:
                                                                                  device=self.device)
             self.altitude = alt.to(self.device, torch.float64).contiguous()
             self._slopes_from(self.altitude)
+        if vegetation is not None or density is not None or dousing is not None:
+            self._pack_layers()
         call("gca_count_cells", dev.ptr(self.grid[self.cur]), E, H, W, self._empty, self._tree, self._fire,
              dev.ptr(self.counts), st)
 
@@ -258,6 +292,13 @@ class AdvancedForestFireBulldozerEnv:
         """The CA step alone (RepeatCAJax's one step) for every env; swaps the ping-pong buffers."""
         E, H, W = self.num_envs, self.nrows, self.ncols
         a, b = self.cur, 1 - self.cur
+        if self.slope_layout == "packed":
+            call("gca_alex_step_packed", self.alex_params, E, H, W, dev.ptr(self.grid[a]), dev.ptr(self.grid[b]),
+                 dev.ptr(self.age[a]), dev.ptr(self.age[b]), dev.ptr(self.vd), dev.ptr(self.dous_bits),
+                 dev.ptr(self.slope_data), dev.ptr(self.wind_index), dev.ptr(self.rng_step), dev.ptr(self.counts),
+                 dev.stream_ptr(self.device))
+            self.cur = b
+            return
         fn = "gca_alex_step_es" if self.slope_layout == "edge" else "gca_alex_step"
         call(fn, self.alex_params, E, H, W, dev.ptr(self.grid[a]), dev.ptr(self.grid[b]),
              dev.ptr(self.age[a]), dev.ptr(self.age[b]), dev.ptr(self.vegetation), dev.ptr(self.density),
@@ -274,10 +315,7 @@ class AdvancedForestFireBulldozerEnv:
         full = full.to(torch.int32).reshape(E, -1).contiguous()
         a = full[:, :2].contiguous()
         self.ca_step()
-        call("gca_advenv_post", self.env_params, dev.ptr(a), dev.ptr(self.pos), dev.ptr(self.accu),
-             dev.ptr(self.wind_index), dev.ptr(self.time_step), dev.ptr(self.is_night), dev.ptr(self.dousing), H, W,
-             dev.ptr(self.counts), dev.ptr(self.rng_step), dev.ptr(self.reward), dev.ptr(self.done), E,
-             dev.stream_ptr(self.device))
+        self.post_step(a)
         if self.rgb is not None:
             self.render_observation(full)
         self.steps_elapsed += 1
@@ -286,6 +324,14 @@ class AdvancedForestFireBulldozerEnv:
         return self._obs(), self.reward, terminated, torch.zeros_like(terminated), self._info()
 
     stateless_step = step
+
+    def post_step(self, action2):
+        """gca_advenv_post for (E, 2) int32 device actions: wind change, time, Move/Modify, reward, done."""
+        E, H, W = self.num_envs, self.nrows, self.ncols
+        call("gca_advenv_post", self.env_params, dev.ptr(action2), dev.ptr(self.pos), dev.ptr(self.accu),
+             dev.ptr(self.wind_index), dev.ptr(self.time_step), dev.ptr(self.is_night), dev.ptr(self.dousing),
+             dev.ptr(self.dous_bits), H, W, dev.ptr(self.counts), dev.ptr(self.rng_step), dev.ptr(self.reward),
+             dev.ptr(self.done), E, dev.stream_ptr(self.device))
 
     def conditional_reset(self):
         """Re-inject the initial state of terminated envs (:422-518); time_step/is_night are kept."""
@@ -302,7 +348,8 @@ class AdvancedForestFireBulldozerEnv:
         t, f = self.counts[:, 1].float(), self.counts[:, 2].float()
         self.reward.copy_(torch.where(mask, -(f / (t + f + 1e-8)), self.reward))
         call("gca_reset_where", dev.ptr(self.done), E, H, W, dev.ptr(self.grid[self.cur]), dev.ptr(init["grid"]),
-             dev.ptr(self.age[self.cur]), dev.ptr(init["age"]), dev.ptr(self.dousing), None, dev.ptr(self.pos),
+             dev.ptr(self.age[self.cur]), dev.ptr(init["age"]), dev.ptr(self.dousing), None,
+             dev.ptr(self.dous_bits), dev.ptr(self.pos),
              dev.ptr(init["pos"]), dev.ptr(self.accu), dev.ptr(self.wind_index), dev.ptr(init["wind_index"]),
              dev.stream_ptr(self.device))
         return self._obs(), self.reward, self.done.bool(), torch.zeros_like(mask), self._info()

@@ -164,6 +164,22 @@ int gca_alex_step_es(const gca_alex_params* p, int E, int H, int W, const uint8_
                      const uint32_t* rng_step, const float* inj_burn, const float* inj_grow, const int32_t* inj_age,
                      float* prob_out, int32_t* counts, void* stream);
 
+/* gca_alex_step_es on the Advanced env's packed layout (Philox mode, W % 256 == 0, H % 16 == 0, 16-B aligned
+ * arrays): vd[e][r][c] = min(veg, 7) | min(den, 7) << 4; dous_bits[e][r][c / 16] bit c % 16 = (dousing != 0)
+ * (the env's dousing counts are 0/1: ModifyJax writes 1, move_modify_jax.py:102-114); edge_slope_coal = the edge
+ * layout with every 256-column row segment of a plane in coalesced order (gca_alex_edge_slope_coalesce).
+ * Results are bit-identical to gca_alex_step_es on the unpacked arrays. Same replaced code as gca_alex_step. */
+int gca_alex_step_packed(const gca_alex_params* p, int E, int H, int W, const uint8_t* grid_in, uint8_t* grid_out,
+                         const int16_t* age_in, int16_t* age_out, const uint8_t* vd, const uint16_t* dous_bits,
+                         const float* edge_slope_coal, const int32_t* wind_index, const uint32_t* rng_step,
+                         int32_t* counts, void* stream);
+/* vd (nullable) and dous_bits of gca_alex_step_packed from veg / den / dousing (E,H,W) u8; W % 16 == 0. */
+int gca_alex_pack_layers(const uint8_t* veg, const uint8_t* den, const uint8_t* dousing, uint8_t* vd,
+                         uint16_t* dous_bits, int E, int H, int W, void* stream);
+/* edge_slope (E,4,H,W) -> coalesced order: inside every 256-column segment of a row, column 16q + 4m + j moves
+ * to position 64m + 4q + j (W % 256 == 0). */
+int gca_alex_edge_slope_coalesce(const float* edge_slope, float* edge_slope_coal, int E, int H, int W, void* stream);
+
 /* Edge-slope layout for gca_alex_step_es from altitude [E][H][W] f64 (NULL = flat): edge_slope[e][k][r][c] =
  * V = +exp_f32(a) if a >= 0 else -exp_f32(-a), a = 0.078f * s, s = f32(degrees(atan((alt[r][c] - alt[n]) /
  * (1.414 if diagonal)))) toward neighbour n = k-th of (-1,-1), (-1,0), (-1,+1), (0,-1) (s = 0 where n is
@@ -214,17 +230,19 @@ typedef struct {
 /* After gca_alex_step: wind change (repeat: ca_alexandridis_jax.py:442-451), time
  * accumulation (repeat_ca_jax.py:191-198, f32), MoveJax, ModifyJax (dousing[r][c] = 1
  * if shoot==1), time_step += 1, is_night toggle, reward = -(f/(t+f+1e-8)) f32,
- * done = no fire, rng_step += 1.                                                  */
+ * done = no fire, rng_step += 1. dous_bits (nullable): the packed layout's dousing bits, set with dousing. */
 int gca_advenv_post(const gca_advenv_params* p, const int32_t* action, int32_t* pos, float* accu,
-                    int32_t* wind_index, int32_t* time_step, int32_t* is_night, uint8_t* dousing, int H, int W,
-                    const int32_t* counts, uint32_t* rng_step, float* reward, uint8_t* done, int E, void* stream);
+                    int32_t* wind_index, int32_t* time_step, int32_t* is_night, uint8_t* dousing, uint16_t* dous_bits,
+                    int H, int W, const int32_t* counts, uint32_t* rng_step, float* reward, uint8_t* done, int E,
+                    void* stream);
 
 /* conditional_reset (advanced_bulldozer.py:422-518): envs with done[e] copy their
- * initial grid/age/dousing/position/time/wind_index (and clear done).            */
+ * initial grid/age/dousing/position/time/wind_index (and clear done); dous_bits (nullable, packed layout)
+ * are zeroed (only without dousing0).                                             */
 int gca_reset_where(const uint8_t* done, int E, int H, int W, uint8_t* grid, const uint8_t* grid0,
                     int16_t* age, const int16_t* age0, uint8_t* dousing, const uint8_t* dousing0,
-                    int32_t* pos, const int32_t* pos0, float* accu, int32_t* wind_index, const int32_t* wind_index0,
-                    void* stream);
+                    uint16_t* dous_bits, int32_t* pos, const int32_t* pos0, float* accu, int32_t* wind_index,
+                    const int32_t* wind_index0, void* stream);
 
 /* ------------------------------------------- Advanced env observations (RGB)
  * MDP.build_observation_on_extensions + grid_to_rgb_with_extensions + grid_to_rgb

@@ -206,3 +206,83 @@ def test_env_edge_and_planes_layouts_agree(device):
         outs = [env.step(act) for env in envs]
         assert np.array_equal(outs[0][0][0].cpu().numpy(), outs[1][0][0].cpu().numpy())
         assert np.array_equal(outs[0][1].cpu().numpy(), outs[1][1].cpu().numpy())
+
+
+def packed_step(device, p, case, es, rng_step):
+    """gca_alex_step_packed on the packed layers built by the library from the case's u8 layers."""
+    import torch
+
+    from gymca_amd import _device as dev
+    from gymca_amd._lib import call
+
+    E, H, W = case["grid"].shape
+    g, a = _t(case["grid"], torch.uint8, device), _t(case["age"], torch.int16, device)
+    veg, den, dous = (_t(case[k], torch.uint8, device) for k in ("veg", "den", "dous"))
+    vd = torch.empty_like(veg)
+    bits = torch.empty((E, H * W // 16), dtype=torch.int16, device=device)
+    call("gca_alex_pack_layers", dev.ptr(veg), dev.ptr(den), dev.ptr(dous), dev.ptr(vd), dev.ptr(bits), E, H, W,
+         dev.stream_ptr())
+    coal = torch.empty_like(es)
+    call("gca_alex_edge_slope_coalesce", dev.ptr(es), dev.ptr(coal), E, H, W, dev.stream_ptr())
+    wi = _t(case["widx"], torch.int32, device)
+    rs = _t(np.asarray(rng_step, np.uint32).view(np.int32), torch.int32, device)
+    go, ao = torch.empty_like(g), torch.empty_like(a)
+    counts = torch.zeros((E, 3), dtype=torch.int32, device=device)
+    call("gca_alex_step_packed", p, E, H, W, dev.ptr(g), dev.ptr(go), dev.ptr(a), dev.ptr(ao), dev.ptr(vd),
+         dev.ptr(bits), dev.ptr(coal), dev.ptr(wi), dev.ptr(rs), dev.ptr(counts), dev.stream_ptr())
+    return go.cpu().numpy(), ao.cpu().numpy(), counts.cpu().numpy(), coal.cpu().numpy(), bits.cpu().numpy()
+
+
+@pytest.mark.parametrize("E,H,W,seed", [(2, 256, 256, 31), (1, 48, 512, 32), (1, 32, 1024, 33), (1, 512, 512, 34)])
+def test_packed_step_bit_exact_vs_edge(device, E, H, W, seed):
+    """The packed env layout (vd byte, dousing bits, coalesced edge slopes) reproduces gca_alex_step_es bit for
+    bit over several steps, and the layout builders match their definitions."""
+    case = make_case(E, H, W, seed, p_tree=0.01, dousing_p=0.2)
+    p = params(H, 0.01, seed=seed * 7)
+    es, _ = slopes(device, altitude(E, H, W, seed))
+    es_np = es.cpu().numpy()
+    for s in range(3):
+        rs = np.full(E, 5 * s + 1, np.uint32)
+        g1, a1, c1, coal, bits = packed_step(device, p, case, es, rs)
+        g0, a0, c0, _ = step(device, "gca_alex_step_es", p, case, es, rng_step=rs)
+        assert np.array_equal(g1, g0), f"step {s}: {np.argwhere(g1 != g0)[:5]}"
+        assert np.array_equal(a1, a0) and np.array_equal(c1, c0)
+        if s == 0:
+            c = np.arange(W) % 256
+            pos = (np.arange(W) // 256) * 256 + 64 * ((c >> 2) & 3) + 4 * (c >> 4) + (c & 3)
+            want = np.empty_like(es_np)
+            want[..., pos] = es_np
+            assert np.array_equal(coal, want)
+            d = case["dous"].reshape(E, H * W // 16, 16).astype(np.uint32)
+            assert np.array_equal(bits.view(np.uint16), (d << np.arange(16, dtype=np.uint32)).sum(-1).astype(np.uint16))
+        case["grid"], case["age"] = g1, a1
+
+
+def test_env_packed_and_edge_layouts_agree(device):
+    """The env on the packed layout (the default at W % 256 == 0) and on the plain edge layout: identical
+    grids, rewards, dousing and positions over steps with shooting (dousing bits set by gca_advenv_post) and a
+    conditional reset (bits zeroed by gca_reset_where)."""
+    from gymca_amd.forest_fire.bulldozer import AdvancedForestFireBulldozerEnv
+
+    E, N = 3, 256
+    envs = [AdvancedForestFireBulldozerEnv(N, N, key=5, num_envs=E, use_hidden=True, device=device,
+                                           hidden_rng=np.random.RandomState(3), slope_layout=lay)
+            for lay in ("auto", "edge")]
+    assert envs[0].slope_layout == "packed"
+    case = make_case(E, N, N, 19, hidden=False)
+    for env in envs:
+        env.reset()
+        env.set_state(grid=case["grid"], fire_age=case["age"], wind_index=case["widx"])
+        env.pos[:, 0], env.pos[:, 1] = 100, 100  # shoot into the fire region
+    rng = np.random.default_rng(2)
+    for t in range(14):
+        act = np.stack([rng.integers(0, 9, E), rng.integers(0, 2, E)], axis=1)
+        outs = [env.step(act) for env in envs]
+        assert np.array_equal(outs[0][0][0].cpu().numpy(), outs[1][0][0].cpu().numpy()), f"step {t}"
+        assert np.array_equal(outs[0][1].cpu().numpy(), outs[1][1].cpu().numpy())
+        assert np.array_equal(envs[0].dousing.cpu().numpy(), envs[1].dousing.cpu().numpy())
+        if t == 8:
+            for env in envs:
+                env.done[1] = 1
+                env.conditional_reset()
+    assert int(envs[0].dousing.sum()) > 0

@@ -99,7 +99,7 @@ def test_reset_where(device):
     ref = torch.where(done.bool()[:, None, None], g0, g)
     pos = torch.zeros((E, 2), dtype=torch.int32, device=device)
     pos0 = torch.ones((E, 2), dtype=torch.int32, device=device)
-    call("gca_reset_where", dev.ptr(done), E, H, W, dev.ptr(g), dev.ptr(g0), None, None, None, None, dev.ptr(pos),
+    call("gca_reset_where", dev.ptr(done), E, H, W, dev.ptr(g), dev.ptr(g0), None, None, None, None, None, dev.ptr(pos),
          dev.ptr(pos0), None, None, None, dev.stream_ptr())
     assert torch.equal(g, ref) and int(done.sum()) == 0
     assert pos[:, 0].tolist() == [0, 1, 0, 1, 1]
