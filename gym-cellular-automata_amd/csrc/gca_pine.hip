@@ -1,0 +1,125 @@
+// gca_pine.hip — pinecone spotting of the Alexandridis CA on gfx950.
+// Reference: PartiallyObservableForestFireJax._handle_pinecone_spread (ca_alexandridis_jax.py:229-319)
+//            + _compute_pinecone_burn_probability (:208-227) and the scatter of _update_grid (:400-420,
+//            commented out in the reference's live path; enabled here on request).
+//
+// Every cell burning in the step's INPUT grid (fire_mask) throws n = min(Poisson(1), max_pinecones)
+// pinecones. Pinecone m: direction d in [0, 8), thrust t = N(0, 1) * ft[ft_lookup[d]] (the env's current
+// wind ft matrix), landing (clip(round(r + dx[d] t)), clip(round(c + dy[d] t))). A pinecone landing on a
+// TREE of the step's OUTPUT grid ignites it with probability 0.48 (1 + p_veg) (1 + p_den) of the target.
+// round(r + dx t) = r + dx * round(t) for dx in {-1, 0, 1} (t continuous), so the kernel draws the integer
+// s = round(t) directly from its exact law P(s = k) = Phi((k + .5) / f) - Phi((k - .5) / f): 32-bit
+// inverse-CDF thresholds built on the host in f64 (gymca_amd/forest_fire/operators/pinecones.py) and one
+// integer compare per threshold, so the C oracle reproduces every landing bit for bit.
+//
+// Draws (Philox4x32-10): block (lin, env, step, PINE) word 0 -> n (Poisson CDF thresholds); block
+// (lin, env, step, PINE + 1 + m) -> s (word 0), burn uniform (word 1 >> 8), direction (word 2 >> 29).
+// Duplicates (the reference's .at[].set scatter leaves their order unspecified): a target ignites iff ANY
+// pinecone landing on it burns; its age is randint(age_lo, age_hi) of word 0 of block (target lin, env,
+// step, PINA), whichever pinecone wins. The ignition is an atomicCAS of the target's byte (TREE -> FIRE),
+// so exactly one thread writes the age and moves one count from tree to fire.
+// Cost: 1 B/cell of input grid read + ~2 Philox blocks per burning cell + scattered byte CAS per landing.
+#include "gca_common.h"
+
+namespace {
+
+__device__ __forceinline__ int cdf_pick(uint32_t x, const uint32_t* thr, int n) {
+    int k = 0;
+    for (int j = 0; j < n; ++j) k += x >= thr[j] ? 1 : 0;
+    return k;
+}
+
+// one thread per 16-cell chunk of the input grid; the loops run only over its burning cells
+__global__ __launch_bounds__(256) void alex_pinecones_kernel(gca_pine_params p, int H, int W,
+                                                             const uint8_t* __restrict__ grid_in,
+                                                             uint8_t* __restrict__ grid_out,
+                                                             int16_t* __restrict__ age_out,
+                                                             const uint8_t* __restrict__ veg,
+                                                             const uint8_t* __restrict__ den,
+                                                             const int32_t* __restrict__ wind_index,
+                                                             const uint32_t* __restrict__ s_cdf,
+                                                             const uint32_t* __restrict__ rng_step,
+                                                             int32_t* __restrict__ counts, int64_t chunks_per_env,
+                                                             int E) {
+    const int64_t gch = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int e = (int)(gch / chunks_per_env);
+    if (e >= E) return;
+    const int64_t ch = gch - (int64_t)e * chunks_per_env;
+    const int64_t HW = (int64_t)H * W;
+    const int64_t c0 = ch * 16;
+    const uint8_t* gi = grid_in + (int64_t)e * HW;
+    uint32_t fire = 0u;
+    for (int i = 0; i < 16; ++i)
+        if (c0 + i < HW && gi[c0 + i] == (uint8_t)p.fire) fire |= 1u << i;
+    if (!fire) return;
+    const uint32_t k0 = (uint32_t)p.seed, k1 = (uint32_t)(p.seed >> 32);
+    const uint32_t env_id = (uint32_t)(p.env_offset + e);
+    const uint32_t step = rng_step ? rng_step[e] : 0u;
+    const uint32_t* tab = s_cdf + (int64_t)wind_index[e] * 8 * GCA_PINE_CDF;
+    uint8_t* go = grid_out + (int64_t)e * HW;
+    const uint8_t* vE = veg + (int64_t)e * HW;
+    const uint8_t* dE = den + (int64_t)e * HW;
+    while (fire) {
+        const int i = __builtin_ctz(fire);
+        fire &= fire - 1u;
+        const uint32_t lin = (uint32_t)(c0 + i);
+        const int r = (int)(lin / (uint32_t)W), c = (int)(lin - (uint32_t)r * (uint32_t)W);
+        const u32x4 B0 = philox4x32_10(u32x4{lin, env_id, step, GCA_TAG_PINE}, k0, k1);
+        const int n = min(cdf_pick(B0.x, p.n_cdf, GCA_PINE_MAX), p.max_pinecones);
+        for (int m = 0; m < n; ++m) {
+            const u32x4 X = philox4x32_10(u32x4{lin, env_id, step, GCA_TAG_PINE + 1u + (uint32_t)m}, k0, k1);
+            const int d = (int)(X.z >> 29);
+            const uint32_t* t = tab + d * GCA_PINE_CDF;  // t[0] = 2K thresholds, then t[1..2K]; s in [-K, K]
+            const int s = cdf_pick(X.x, t + 1, (int)t[0]) - (int)(t[0] >> 1);
+            const int tr = min(max(r + p.dx[d] * s, 0), H - 1), tc = min(max(c + p.dy[d] * s, 0), W - 1);
+            const int64_t tl = (int64_t)tr * W + tc;
+            // the target's pinecone burn probability (:209-227): (0.48 * (1 + p_veg)) * (1 + p_den), clip 1..5
+            const int vv = min(max((int)vE[tl], 1), 5), dd = min(max((int)dE[tl], 1), 5);
+            const float prob = __fmul_rn(__fmul_rn(p.scale, p.veg1p[vv]), p.den1p[dd]);
+            if (!((float)(X.y >> 8) * 0x1.0p-24f < prob)) continue;
+            // TREE -> FIRE on the output grid, once: atomicCAS of the aligned word holding the byte
+            uint8_t* bp = go + tl;
+            uint32_t* wp = reinterpret_cast<uint32_t*>(reinterpret_cast<uintptr_t>(bp) & ~(uintptr_t)3);
+            const uint32_t sh = 8u * (uint32_t)(reinterpret_cast<uintptr_t>(bp) & 3);
+            uint32_t old = __hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            bool won = false;
+            while (((old >> sh) & 0xFFu) == (uint32_t)p.tree) {
+                const uint32_t nw = (old & ~(0xFFu << sh)) | ((uint32_t)p.fire << sh);
+                const uint32_t prev = atomicCAS(wp, old, nw);
+                if (prev == old) {
+                    won = true;
+                    break;
+                }
+                old = prev;
+            }
+            if (won) {
+                const u32x4 A = philox4x32_10(u32x4{(uint32_t)tl, env_id, step, GCA_TAG_PINE_AGE}, k0, k1);
+                age_out[(int64_t)e * HW + tl] = (int16_t)randint_ms(A.x, p.age_lo, p.age_hi);
+                if (counts) {
+                    atomicSub(counts + 3 * e + 1, 1);
+                    atomicAdd(counts + 3 * e + 2, 1);
+                }
+            }
+        }
+    }
+}
+
+}  // namespace
+
+extern "C" int gca_alex_pinecones(const gca_pine_params* p, int E, int H, int W, const uint8_t* grid_in,
+                                  uint8_t* grid_out, int16_t* age_out, const uint8_t* veg, const uint8_t* den,
+                                  const int32_t* wind_index, const uint32_t* s_cdf, const uint32_t* rng_step,
+                                  int32_t* counts, void* stream) {
+    GCA_CHECK_ARG(p && grid_in && grid_out && age_out && veg && den && wind_index && s_cdf,
+                  "alex_pinecones: null argument");
+    GCA_CHECK_ARG(E > 0 && H > 0 && W > 0 && grid_in != grid_out, "alex_pinecones: bad sizes or aliased grids");
+    GCA_CHECK_ARG(p->max_pinecones >= 0 && p->max_pinecones <= GCA_PINE_MAX, "alex_pinecones: max_pinecones in [0, 8]");
+    GCA_CHECK_ARG(((uintptr_t)grid_out & 3u) == 0 && ((int64_t)H * W) % 4 == 0,
+                  "alex_pinecones: grid_out 4-B aligned and H*W % 4 == 0 (byte CAS on whole words)");
+    const int64_t cpe = ((int64_t)H * W + 15) / 16;
+    const int64_t n = cpe * E;
+    hipLaunchKernelGGL(alex_pinecones_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *p,
+                       H, W, grid_in, grid_out, age_out, veg, den, wind_index, s_cdf, rng_step, counts, cpe, E);
+    GCA_CHECK_LAUNCH("alex_pinecones");
+    return GCA_OK;
+}

@@ -21,6 +21,10 @@ TAG_ALEX_WIND = 0x414C5857
 TAG_ACTION = 0x41435449
 TAG_INIT = 0x494E4954
 TAG_DS_CELL = 0x44534345
+TAG_PINE = 0x50494E45
+TAG_PINE_AGE = 0x50494E41
+GCA_PINE_MAX = 8
+GCA_PINE_CDF = 17
 
 
 class GCAError(RuntimeError):
@@ -69,6 +73,27 @@ class AlexParams(ctypes.Structure):
         ("winds", (c_float * 9) * 16),
         ("heat0", c_float),
         ("burnout_eq1", c_int32),
+    ]
+
+
+class PineParams(ctypes.Structure):
+    """gca_pine_params (include/gca.h)."""
+
+    _fields_ = [
+        ("n_cdf", c_uint32 * GCA_PINE_MAX),
+        ("max_pinecones", c_int32),
+        ("dx", c_int32 * 8),
+        ("dy", c_int32 * 8),
+        ("scale", c_float),
+        ("veg1p", c_float * 6),
+        ("den1p", c_float * 6),
+        ("age_lo", c_int32),
+        ("age_hi", c_int32),
+        ("seed", c_uint64),
+        ("env_offset", c_int32),
+        ("empty", c_int32),
+        ("tree", c_int32),
+        ("fire", c_int32),
     ]
 
 
@@ -137,6 +162,7 @@ _SIGNATURES = {
     "gca_alex_step_es": ([POINTER(AlexParams), c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
                          c_int),
     "gca_alex_edge_slope_from_altitude": ([P, P, c_int, c_int, c_int, P], c_int),
+    "gca_alex_pinecones": ([POINTER(PineParams), c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P], c_int),
     "gca_alex_step_packed": ([POINTER(AlexParams), c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, P], c_int),
     "gca_alex_pack_layers": ([P, P, P, P, P, c_int, c_int, c_int, P], c_int),
     "gca_alex_edge_slope_coalesce": ([P, P, c_int, c_int, c_int, P], c_int),

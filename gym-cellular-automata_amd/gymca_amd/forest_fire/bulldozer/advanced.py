@@ -38,7 +38,7 @@ class AdvancedForestFireBulldozerEnv:
     def __init__(self, nrows, ncols, key=0, num_envs=8, speed_move=0.12, speed_act=0.03, speed_multiplier=1.0,
                  pos_bull=None, pos_fire=None, t_move=None, t_shoot=None, t_any=0.001, p_tree=0.90, p_empty=0.10,
                  use_hidden=True, middle_fire=False, enable_extensions=False, device=None, env_offset=0,
-                 hidden_rng=None, slope_layout="auto", observation="grid"):
+                 hidden_rng=None, slope_layout="auto", observation="grid", pinecones=False):
         import torch
 
         self.device = dev.require_device(device)
@@ -75,6 +75,13 @@ class AdvancedForestFireBulldozerEnv:
         mp = make_params(ACTION_SETS)
         ep.up_mask, ep.down_mask, ep.left_mask, ep.right_mask = mp.up_mask, mp.down_mask, mp.left_mask, mp.right_mask
         self.env_params = ep
+        # pinecone spotting after each CA step (ca_alexandridis_jax.py:229-319, :400-420; commented out in the
+        # reference's _update_grid, so off by default): gca_alex_pinecones with the step's wind
+        self.pinecones = bool(pinecones)
+        if self.pinecones:
+            from ..operators.pinecones import make_pine_params, s_cdf_tables
+
+            self.pine_params = make_pine_params(self.key, self._empty, self._tree, self._fire, self.env_offset)
 
         kw = dict(device=self.device)
         self.grid = torch.zeros((2, E, H, W), dtype=torch.uint8, **kw)
@@ -97,6 +104,8 @@ class AdvancedForestFireBulldozerEnv:
         self.vd = torch.zeros((E, H, W), dtype=torch.uint8, **kw) if slope_layout == "packed" else None
         self.dous_bits = torch.zeros((E, H * W // 16), dtype=torch.int16, **kw) if slope_layout == "packed" else None
         self.wind_index = torch.zeros(E, dtype=torch.int32, **kw)
+        self.pine_tables = (torch.as_tensor(s_cdf_tables(self._winds).view(np.int32), **kw) if self.pinecones
+                            else None)
         self.pos = torch.zeros((E, 2), dtype=torch.int32, **kw)
         self.accu = torch.zeros(E, dtype=torch.float32, **kw)
         self.time_step = torch.ones(E, dtype=torch.int32, **kw)
@@ -297,6 +306,7 @@ class AdvancedForestFireBulldozerEnv:
                  dev.ptr(self.age[a]), dev.ptr(self.age[b]), dev.ptr(self.vd), dev.ptr(self.dous_bits),
                  dev.ptr(self.slope_data), dev.ptr(self.wind_index), dev.ptr(self.rng_step), dev.ptr(self.counts),
                  dev.stream_ptr(self.device))
+            self._pinecones(a, b)
             self.cur = b
             return
         fn = "gca_alex_step_es" if self.slope_layout == "edge" else "gca_alex_step"
@@ -304,7 +314,15 @@ class AdvancedForestFireBulldozerEnv:
              dev.ptr(self.age[a]), dev.ptr(self.age[b]), dev.ptr(self.vegetation), dev.ptr(self.density),
              dev.ptr(self.dousing), dev.ptr(self.slope_data), dev.ptr(self.wind_index), dev.ptr(self.rng_step),
              None, None, None, None, dev.ptr(self.counts), dev.stream_ptr(self.device))
+        self._pinecones(a, b)
         self.cur = b
+
+    def _pinecones(self, a, b):
+        if self.pinecones:
+            E, H, W = self.num_envs, self.nrows, self.ncols
+            call("gca_alex_pinecones", self.pine_params, E, H, W, dev.ptr(self.grid[a]), dev.ptr(self.grid[b]),
+                 dev.ptr(self.age[b]), dev.ptr(self.vegetation), dev.ptr(self.density), dev.ptr(self.wind_index),
+                 dev.ptr(self.pine_tables), dev.ptr(self.rng_step), dev.ptr(self.counts), dev.stream_ptr(self.device))
 
     def step(self, action):
         """action: (E, 2) or (E, 3) ints (move, shoot[, extension]); device tensor or numpy."""

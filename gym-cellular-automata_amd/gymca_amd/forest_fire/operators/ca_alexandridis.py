@@ -123,9 +123,11 @@ class PartiallyObservableForestFireJax(Operator):
 
     deterministic = False
 
-    def __init__(self, grid_size, empty, tree, fire, *args, **kwargs):
+    def __init__(self, grid_size, empty, tree, fire, *args, pinecones=False, **kwargs):
         super().__init__(*args, **kwargs)
         self.grid_size = grid_size
+        # pinecone spotting (:229-319, :400-420): commented out in the reference; gca_alex_pinecones here
+        self.pinecones = bool(pinecones)
         c = alex_constants(grid_size)
         self.initial_spread_time = grid_size + (grid_size // 2)
         self.fire_age_min = c["fire_age_min"]
@@ -190,6 +192,13 @@ class PartiallyObservableForestFireJax(Operator):
         call("gca_alex_step", p, E, H, W, dev.ptr(grid_in), dev.ptr(grid_out), dev.ptr(age_in), dev.ptr(age_out),
              dev.ptr(veg), dev.ptr(den), dev.ptr(dous), dev.ptr(p_slope), dev.ptr(widx), dev.ptr(rng_step),
              dev.ptr(inj[0]), dev.ptr(inj[1]), dev.ptr(inj[2]), dev.ptr(probs), None, st)
+        if self.pinecones:  # on the step's output, with the wind of the step (before its change)
+            from .pinecones import make_pine_params, s_cdf_tables
+
+            pp = make_pine_params(seed, self.empty, self.tree, self.fire)
+            tabs = torch.as_tensor(s_cdf_tables(shared_context["winds"]).view(np.int32), device=device)
+            call("gca_alex_pinecones", pp, E, H, W, dev.ptr(grid_in), dev.ptr(grid_out), dev.ptr(age_out),
+                 dev.ptr(veg), dev.ptr(den), dev.ptr(widx), dev.ptr(tabs), dev.ptr(rng_step), None, st)
         new_widx = widx.clone()
         call("gca_alex_wind_change", float(np.float32(shared_context.get("p_wind_change", 0.06))), p.n_winds,
              p.seed, 0, dev.ptr(rng_step), dev.ptr(wu), dev.ptr(wk), dev.ptr(new_widx), E, st)

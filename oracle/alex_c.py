@@ -117,3 +117,27 @@ def wind_change(p_change, n_winds, seed, env_offset, rng_step, wind_index):
     lib().oracle_alex_wind_change(ctypes.c_float(p_change), n_winds, ctypes.c_uint64(seed), env_offset, _p(rs),
                                   _p(wi), len(wi))
     return wi
+
+
+class OraclePineParams(ctypes.Structure):
+    _fields_ = [("n_cdf", ctypes.c_uint32 * 8), ("max_pinecones", ctypes.c_int32), ("dx", ctypes.c_int32 * 8),
+                ("dy", ctypes.c_int32 * 8), ("scale", ctypes.c_float), ("veg1p", ctypes.c_float * 6),
+                ("den1p", ctypes.c_float * 6), ("age_lo", ctypes.c_int32), ("age_hi", ctypes.c_int32),
+                ("seed", ctypes.c_uint64), ("env_offset", ctypes.c_int32), ("empty", ctypes.c_int32),
+                ("tree", ctypes.c_int32), ("fire", ctypes.c_int32)]
+
+
+def pinecones(params, grid_in, grid_out, age_out, veg, den, wind_index, s_cdf, rng_step=None, counts=None):
+    """oracle_alex_pinecones on copies of grid_out / age_out / counts; params: a field-compatible struct
+    (the product's PineParams). Returns (grid_out, age_out, counts)."""
+    o = OraclePineParams()
+    ctypes.memmove(ctypes.addressof(o), ctypes.addressof(params), ctypes.sizeof(o))
+    E, H, W = grid_in.shape
+    c = lambda a, t: np.ascontiguousarray(a, dtype=t)
+    gi, go, ao = c(grid_in, np.uint8), c(grid_out, np.uint8).copy(), c(age_out, np.int16).copy()
+    veg, den, wi, sc = c(veg, np.uint8), c(den, np.uint8), c(wind_index, np.int32), c(s_cdf, np.uint32)
+    rs = None if rng_step is None else c(rng_step, np.uint32)
+    cn = None if counts is None else c(counts, np.int32).copy()
+    lib().oracle_alex_pinecones(ctypes.byref(o), E, H, W, _p(gi), _p(go), _p(ao), _p(veg), _p(den), _p(wi), _p(sc),
+                                _p(rs), _p(cn))
+    return go, ao, cn

@@ -254,3 +254,78 @@ void oracle_alex_wind_change(float p_change, int n_winds, uint64_t seed, int env
         if (u01(x[0]) < p_change) wind_index[e] = (wind_index[e] + randint_ms(x[1], 1, 8)) % n_winds;
     }
 }
+
+/* ------------------------------------------------------------------ pinecone spotting
+ * Restates ca_alexandridis_jax.py:229-319 + the scatter of :400-420 with the device's draw convention
+ * (gca_pine.hip): every FIRE cell of grid_in (row-major) throws n = min(Poisson(1), max) pinecones; pinecone m
+ * lands at (clip(r + dx[d] s), clip(c + dy[d] s)) and, if that cell of grid_out is TREE and u < prob, ignites
+ * it with age randint(age_lo, age_hi) of the target's own draw. Sequential application = the device's
+ * any-pinecone-ignites rule (an ignited target is no longer TREE). */
+#define PINE_MAX 8
+#define PINE_CDF 17
+#define TAG_PINE 0x50494E45u
+#define TAG_PINE_AGE 0x50494E41u
+typedef struct {
+    uint32_t n_cdf[PINE_MAX];
+    int32_t max_pinecones;
+    int32_t dx[8], dy[8];
+    float scale;
+    float veg1p[6], den1p[6];
+    int32_t age_lo, age_hi;
+    uint64_t seed;
+    int32_t env_offset;
+    int32_t empty, tree, fire;
+} oracle_pine_params;
+
+static int cdf_pick(uint32_t x, const uint32_t* thr, int n) {
+    int k = 0;
+    for (int j = 0; j < n; ++j) k += x >= thr[j];
+    return k;
+}
+
+void oracle_alex_pinecones(const oracle_pine_params* p, int E, int H, int W, const uint8_t* grid_in, uint8_t* grid_out,
+                           int16_t* age_out, const uint8_t* veg, const uint8_t* den, const int32_t* wind_index,
+                           const uint32_t* s_cdf, const uint32_t* rng_step, int32_t* counts) {
+    const long HW = (long)H * W;
+    const uint32_t k0 = (uint32_t)p->seed, k1 = (uint32_t)(p->seed >> 32);
+    for (int e = 0; e < E; ++e) {
+        const uint32_t env_id = (uint32_t)(p->env_offset + e), step = rng_step ? rng_step[e] : 0u;
+        const uint32_t* tab = s_cdf + (long)wind_index[e] * 8 * PINE_CDF;
+        for (long lin = 0; lin < HW; ++lin) {
+            if (grid_in[e * HW + lin] != p->fire) continue;
+            const int r = (int)(lin / W), c = (int)(lin % W);
+            uint32_t b0[4];
+            const uint32_t c0[4] = {(uint32_t)lin, env_id, step, TAG_PINE};
+            philox(c0, k0, k1, b0);
+            int n = cdf_pick(b0[0], p->n_cdf, PINE_MAX);
+            if (n > p->max_pinecones) n = p->max_pinecones;
+            for (int m = 0; m < n; ++m) {
+                uint32_t x[4];
+                const uint32_t cm[4] = {(uint32_t)lin, env_id, step, TAG_PINE + 1u + (uint32_t)m};
+                philox(cm, k0, k1, x);
+                const int d = (int)(x[2] >> 29);
+                const uint32_t* t = tab + d * PINE_CDF;
+                const int s = cdf_pick(x[0], t + 1, (int)t[0]) - (int)(t[0] >> 1);
+                int tr = r + p->dx[d] * s, tc = c + p->dy[d] * s;
+                tr = tr < 0 ? 0 : (tr > H - 1 ? H - 1 : tr);
+                tc = tc < 0 ? 0 : (tc > W - 1 ? W - 1 : tc);
+                const long tl = (long)tr * W + tc;
+                int vv = veg[e * HW + tl], dd = den[e * HW + tl];
+                vv = vv < 1 ? 1 : (vv > 5 ? 5 : vv);
+                dd = dd < 1 ? 1 : (dd > 5 ? 5 : dd);
+                const float prob = (p->scale * p->veg1p[vv]) * p->den1p[dd];
+                if (!(u01(x[1]) < prob)) continue;
+                if (grid_out[e * HW + tl] != p->tree) continue;
+                grid_out[e * HW + tl] = (uint8_t)p->fire;
+                uint32_t a[4];
+                const uint32_t ca[4] = {(uint32_t)tl, env_id, step, TAG_PINE_AGE};
+                philox(ca, k0, k1, a);
+                age_out[e * HW + tl] = (int16_t)randint_ms(a[0], p->age_lo, p->age_hi);
+                if (counts) {
+                    counts[3 * e + 1] -= 1;
+                    counts[3 * e + 2] += 1;
+                }
+            }
+        }
+    }
+}

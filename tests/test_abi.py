@@ -65,6 +65,9 @@ int main(void) {
   printf("gca_obs_params %zu\n", sizeof(gca_obs_params));
   P(gca_obs_params, ext_skip_blur) P(gca_obs_params, day_length) P(gca_obs_params, color_night)
   P(gca_obs_params, tint_night) P(gca_obs_params, ext_lookup)
+  printf("gca_pine_params %zu\n", sizeof(gca_pine_params));
+  P(gca_pine_params, max_pinecones) P(gca_pine_params, dy) P(gca_pine_params, scale) P(gca_pine_params, den1p)
+  P(gca_pine_params, seed) P(gca_pine_params, fire)
   return 0;
 }
 """
@@ -80,7 +83,8 @@ def test_struct_layouts_match_the_header(tmp_path):
     out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
     got = dict(line.rsplit(" ", 1) for line in out if line)
     py = {"gca_bulldozer_params": _lib.BulldozerParams, "gca_alex_params": _lib.AlexParams,
-          "gca_advenv_params": _lib.AdvEnvParams, "gca_obs_params": _lib.ObsParams}
+          "gca_advenv_params": _lib.AdvEnvParams, "gca_obs_params": _lib.ObsParams,
+          "gca_pine_params": _lib.PineParams}
     for key, val in got.items():
         if "." in key:
             t, f = key.split(".")

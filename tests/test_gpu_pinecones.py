@@ -1,0 +1,75 @@
+"""GPU parity of pinecone spotting (gca_alex_pinecones, ca_alexandridis_jax.py:229-319 + the scatter of
+:400-420): bit-exact against the C oracle (itself checked against the literal restatement of
+_handle_pinecone_spread in tests/test_pinecones_oracle.py), and the env / operator wiring."""
+import numpy as np
+import pytest
+
+from alex_cases import make_case, winds
+from oracle import alex_c
+
+pytestmark = pytest.mark.gpu
+
+
+def _t(x, dtype, device):
+    import torch
+
+    return torch.as_tensor(np.ascontiguousarray(x), device=device).to(dtype).contiguous()
+
+
+@pytest.mark.parametrize("E,H,W,seed", [(2, 24, 24, 1), (1, 40, 36, 2), (2, 64, 64, 3), (1, 256, 256, 4),
+                                        (3, 48, 512, 5)])
+def test_pinecones_bit_exact_vs_oracle(device, E, H, W, seed):
+    import torch
+
+    from gymca_amd import _device as dev
+    from gymca_amd._lib import call
+    from gymca_amd.forest_fire.operators.ca_alexandridis import make_alex_params
+    from gymca_amd.forest_fire.operators.pinecones import make_pine_params, s_cdf_tables
+
+    case = make_case(E, H, W, seed, fire_p=0.15)
+    p, _ = make_alex_params(H, 0, 1, 2, winds(), 0.0, 5 + seed)
+    rs = np.full(E, 11, np.uint32)
+    g1, a1, c1, _ = alex_c.alex_step(p, case["grid"], case["age"], case["veg"], case["den"], case["dous"],
+                                     alex_c.prepare_slope(case["slope"]), case["widx"], rng_step=rs)
+    pp = make_pine_params(1234 + seed, 0, 1, 2, env_offset=3)
+    tabs = s_cdf_tables(winds())
+    want_g, want_a, want_c = alex_c.pinecones(pp, case["grid"], g1, a1, case["veg"], case["den"], case["widx"], tabs,
+                                              rs, c1)
+    gi = _t(case["grid"], torch.uint8, device)
+    go, ao = _t(g1, torch.uint8, device), _t(a1, torch.int16, device)
+    veg, den = _t(case["veg"], torch.uint8, device), _t(case["den"], torch.uint8, device)
+    wi = _t(case["widx"], torch.int32, device)
+    tb = _t(tabs.view(np.int32), torch.int32, device)
+    rsd = _t(rs.view(np.int32), torch.int32, device)
+    counts = _t(c1, torch.int32, device)
+    call("gca_alex_pinecones", pp, E, H, W, dev.ptr(gi), dev.ptr(go), dev.ptr(ao), dev.ptr(veg), dev.ptr(den),
+         dev.ptr(wi), dev.ptr(tb), dev.ptr(rsd), dev.ptr(counts), dev.stream_ptr())
+    assert np.array_equal(go.cpu().numpy(), want_g)
+    assert np.array_equal(ao.cpu().numpy(), want_a)
+    assert np.array_equal(counts.cpu().numpy(), want_c)
+    assert (want_g != g1).sum() > 0
+
+
+def test_env_pinecones_ignite_only_trees(device):
+    """pinecones=True: the same step as pinecones=False plus ignitions of TREE cells; fused counts stay the
+    grid's counts."""
+    import torch
+
+    from gymca_amd import _device as dev
+    from gymca_amd._lib import call
+    from gymca_amd.forest_fire.bulldozer import AdvancedForestFireBulldozerEnv
+
+    E, N = 2, 256
+    envs = [AdvancedForestFireBulldozerEnv(N, N, key=9, num_envs=E, use_hidden=False, device=device, pinecones=pc)
+            for pc in (True, False)]
+    case = make_case(E, N, N, 41, hidden=False)
+    for env in envs:
+        env.reset()
+        env.set_state(grid=case["grid"], fire_age=case["age"], wind_index=case["widx"])
+    act = np.zeros((E, 2), np.int64)
+    g = [env.step(act)[0][0].cpu().numpy() for env in envs]
+    diff = g[0] != g[1]
+    assert diff.sum() > 0 and np.all(g[1][diff] == 1) and np.all(g[0][diff] == 2)
+    cnt = torch.zeros((E, 3), dtype=torch.int32, device=device)
+    call("gca_count_cells", dev.ptr(envs[0].grid[envs[0].cur]), E, N, N, 0, 1, 2, dev.ptr(cnt), dev.stream_ptr())
+    assert torch.equal(cnt, envs[0].counts)
