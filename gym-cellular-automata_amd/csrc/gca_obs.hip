@@ -10,7 +10,8 @@
 //      (H, W, 3 + n_ext) stack, and the row index found is then used as the channel index (clamped to
 //      the last channel, like JAX's out-of-bounds gather). Every block of the env repeats this scan;
 //      it normally ends at row 0;
-//   B. the block's rows (+1 halo row each side) staged in LDS for the blur, then per cell the display
+//   B. the block's rows (+1 halo row each side) and its dousing rows staged in LDS (all loads in one
+//      batch; the render rounds then read LDS only), then per cell the display
 //      value and its f32 RGB: empty/tree/fire colour of the pre-step day/night, the water tint blended
 //      in where dousing_count == 1 (rgb*0.25 + tint*0.75 — exact in f32 for these integer colours, so
 //      the order of the reference's ops cannot matter), the position colour on the bulldozer's cell;
@@ -97,7 +98,8 @@ __global__ __launch_bounds__(256) void adv_observation_kernel(gca_obs_params p, 
                                                               const int32_t* __restrict__ time_step,
                                                               const int32_t* __restrict__ action, int action_stride,
                                                               float* __restrict__ rgb, uint8_t* __restrict__ channels) {
-    extern __shared__ uint8_t T[];  // [(RB + 2) * W]
+    extern __shared__ uint8_t T[];  // [(RB + 2) * W] grid rows r0-1 .. r0+RB (edge-clamped), then [RB * W] dousing
+    uint8_t* D = T + (RB + 2) * W;
     const int e = blockIdx.x / blocks_per_env;
     const int r0 = (blockIdx.x - e * blocks_per_env) * RB;
     const int rows = min(RB, H - r0);
@@ -155,15 +157,37 @@ __global__ __launch_bounds__(256) void adv_observation_kernel(gca_obs_params p, 
         return;
     }
 
-    // ---- stage rows [r0 - 1, r0 + rows] (clamped: edge padding) for the blur
-    if (k.need_blur) {
-        if ((W & 3) == 0) {
+    // ---- stage grid rows [r0 - 1, r0 + rows] (clamped: edge padding, for the blur) and the block's dousing
+    //      rows in LDS, every load issued before any is used: the render rounds below then read LDS only
+    //      and never wait on HBM between their stores
+    const bool stage_all = (W & 3) == 0;  // the 4-cells-per-thread path reads both arrays from LDS
+    if (stage_all || k.need_blur) {
+        const bool al16 = ((((uintptr_t)grid) | ((uintptr_t)dousing)) & 15u) == 0;
+        if ((W & 15) == 0 && al16) {
+            const int w16 = W >> 4;
+            const int ng = (rows + 2) * w16, nd = du ? rows * w16 : 0;
+            for (int idx = threadIdx.x; idx < ng + nd; idx += blockDim.x) {
+                if (idx < ng) {
+                    const int lr = idx / w16, cq = idx - lr * w16;
+                    const int r = min(max(r0 - 1 + lr, 0), H - 1);
+                    reinterpret_cast<uint4*>(T)[lr * w16 + cq] = reinterpret_cast<const uint4*>(g + (int64_t)r * W)[cq];
+                } else {
+                    const int j = idx - ng;
+                    reinterpret_cast<uint4*>(D)[j] = reinterpret_cast<const uint4*>(du + (int64_t)r0 * W)[j];
+                }
+            }
+        } else if (stage_all) {
             const int wq = W >> 2;
-            for (int idx = threadIdx.x; idx < (rows + 2) * wq; idx += blockDim.x) {
-                const int lr = idx / wq, cq = idx - lr * wq;
-                const int r = min(max(r0 - 1 + lr, 0), H - 1);
-                reinterpret_cast<uint32_t*>(T)[lr * wq + cq] =
-                    reinterpret_cast<const uint32_t*>(g + (int64_t)r * W)[cq];
+            const int ng = (rows + 2) * wq, nd = du ? rows * wq : 0;
+            for (int idx = threadIdx.x; idx < ng + nd; idx += blockDim.x) {
+                if (idx < ng) {
+                    const int lr = idx / wq, cq = idx - lr * wq;
+                    const int r = min(max(r0 - 1 + lr, 0), H - 1);
+                    reinterpret_cast<uint32_t*>(T)[lr * wq + cq] = reinterpret_cast<const uint32_t*>(g + (int64_t)r * W)[cq];
+                } else {
+                    const int j = idx - ng;
+                    reinterpret_cast<uint32_t*>(D)[j] = reinterpret_cast<const uint32_t*>(du + (int64_t)r0 * W)[j];
+                }
             }
         } else {
             for (int idx = threadIdx.x; idx < (rows + 2) * W; idx += blockDim.x) {
@@ -192,8 +216,8 @@ __global__ __launch_bounds__(256) void adv_observation_kernel(gca_obs_params p, 
             if (idx < rows * wq) {
                 const int lr = idx / wq, c0 = (idx - lr * wq) * 4, r = r0 + lr;
                 const int64_t cell0 = (int64_t)r * W + c0;
-                const uint32_t gw = *reinterpret_cast<const uint32_t*>(g + cell0);
-                const uint32_t dw = du ? *reinterpret_cast<const uint32_t*>(du + cell0) : 0u;
+                const uint32_t gw = *reinterpret_cast<const uint32_t*>(T + (lr + 1) * W + c0);
+                const uint32_t dw = du ? *reinterpret_cast<const uint32_t*>(D + lr * W + c0) : 0u;
                 // blur of the 4 cells: column sums of columns c0-1 .. c0+4 over the 3 staged rows
                 // (one aligned word + the two edge bytes per row; edge padding at the grid border)
                 int bl4[4] = {0, 0, 0, 0};
@@ -287,9 +311,9 @@ extern "C" int gca_adv_observation(const gca_obs_params* p, int mode, int E, int
     GCA_CHECK_ARG(W <= 16384, "adv_observation: W <= 16384");
     GCA_CHECK_ARG(((uintptr_t)rgb & 15u) == 0 && ((uintptr_t)grid & 3u) == 0 && ((uintptr_t)dousing & 3u) == 0,
                   "adv_observation: rgb must be 16-B and grid/dousing 4-B aligned");
-    const int RB = max(1, min(16, 49152 / W - 2));  // rows per block; (RB + 2) * W bytes of LDS
+    const int RB = max(1, min(16, 32768 / W - 1));  // rows per block; (2 RB + 2) * W bytes of LDS (grid + dousing)
     const int bpe = (H + RB - 1) / RB;
-    hipLaunchKernelGGL(adv_observation_kernel, dim3((unsigned)((int64_t)E * bpe)), dim3(256), (size_t)(RB + 2) * W,
+    hipLaunchKernelGGL(adv_observation_kernel, dim3((unsigned)((int64_t)E * bpe)), dim3(256), (size_t)(2 * RB + 2) * W,
                        (hipStream_t)stream, *p, mode, H, W, RB, bpe, grid, dousing, pos, is_night, time_step, action,
                        action_stride, rgb, channels);
     GCA_CHECK_LAUNCH("adv_observation");
