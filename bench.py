@@ -7,7 +7,7 @@ Alexandridis rule, E = 4096 envs per GPU, N = 256, use_hidden=False (veg = den =
 altitude 0 -> p_slope = 1, still read from HBM every step), mid-episode synthetic state
 (grid iid {EMPTY .1, TREE .8, FIRE .1}, fire ages iid [1, 672], wind_index iid [0, 8)),
 p_tree = 0, p_wind_change = 0.06. One timed step = random actions (device Philox) +
-the CA step (gca_alex_step_es: edge-slope layout, 25 B/cell) + the env step (gca_advenv_post) [+ one RCCL all_gather of the
+the CA step (gca_alex_step_packed: packed edge-slope layout, 23.1 B/cell moved) + the env step (gca_advenv_post) [+ one RCCL all_gather of the
 per-env done mask / reward when --gpus > 1]. Weak scaling: every rank owns E envs.
 
 Also reported: the WindyForestFire bulldozer env (config 2, E = 1024) as `secondary`,
@@ -40,7 +40,9 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=40)
-    ap.add_argument("--warmup", type=int, default=5)
+    # 20 untimed steps: the first ~15 launches of a fresh process run up to 25% slower (clock / TLB warm-up,
+    # profiles/r01l kernel trace), so a short warm-up would fold that ramp into the timed mean
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--gather", choices=["step", "none"], default="step")
@@ -543,7 +545,8 @@ def main():
                          "moved_gbs": alex["achieved_gbs"],
                          "moved_frac": alex["achieved_gbs"] / HBM_PEAK_GBS,
                          "traffic_bytes_per_cell": traffic / (args.envs * args.size * args.size) if traffic else None,
-                         "device_copy_gbs": copy_gbs},
+                         "device_copy_gbs": copy_gbs,
+                         "moved_frac_of_device_copy": alex["achieved_gbs"] / copy_gbs},
             "cpu_baseline": cpu,
             "secondary": secondary,
             "config4": config4,

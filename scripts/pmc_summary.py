@@ -33,6 +33,21 @@ def short(name):
     return None
 
 
+def timed_means(prof_dir, skip=20):
+    """Per-kernel mean duration (us) over the launches after the first `skip` of each kernel (the bench's
+    untimed warm-up steps), from the kernel trace of the same run."""
+    path = os.path.join(prof_dir, "trace", "run_kernel_trace.csv")
+    if not os.path.exists(path):
+        return {}
+    per = defaultdict(list)
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            s = short(row["Kernel_Name"])
+            if s:
+                per[s].append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e3)
+    return {s: sum(v[skip:]) / len(v[skip:]) for s, v in per.items() if len(v) > skip}
+
+
 def main(prof_dir, tag, out_dir="profiles"):
     os.makedirs(out_dir, exist_ok=True)
     stats = os.path.join(prof_dir, "trace", "run_kernel_stats.csv")
@@ -59,11 +74,15 @@ def main(prof_dir, tag, out_dir="profiles"):
              "Source: `bash scripts/profile.sh " + tag + "` on one MI355X (bench.py workload; kernel trace + stats in one "
              "run, each PMC group in its own run). Durations from the --stats pass; counters are per-launch means.",
              "HBM bytes = 2*FETCH_SIZE + WRITE_SIZE (KB units, gfx950 half-counting of 16-B reads).", "",
-             "| kernel | calls | avg us | grid | LDS | scratch | VGPR | SGPR |", "|---|---|---|---|---|---|---|---|"]
+             "`avg us (timed)` = mean over the launches after the 20 warm-up steps (kernel trace), the figure to compare",
+             "with bench.py's kernel_ms; `avg us` = the --stats mean over all launches.", "",
+             "| kernel | calls | avg us | avg us (timed) | grid | LDS | scratch | VGPR | SGPR |",
+             "|---|---|---|---|---|---|---|---|---|"]
+    tm = timed_means(prof_dir)
     for s in sorted(set(dur) | set(meta)):
         c, us = dur.get(s, (0, float("nan")))
         g, lds, scr, v, sg = meta.get(s, (0, 0, 0, 0, 0))
-        lines.append(f"| {s} | {c} | {us:.1f} | {g} | {lds} | {scr} | {v} | {sg} |")
+        lines.append(f"| {s} | {c} | {us:.1f} | {tm.get(s, float('nan')):.1f} | {g} | {lds} | {scr} | {v} | {sg} |")
     lines += ["", "| kernel | counter | mean per launch |", "|---|---|---|"]
     traffic = {}
     for s in sorted(vals):

@@ -149,14 +149,16 @@ def test_dropin_operator_with_reference_draws(device):
     assert ctx2["rng_step"] == 1
 
 
-def test_advanced_env_matches_oracle_composition(device):
+@pytest.mark.parametrize("N", [64, 256])  # 64: edge layout; 256: the packed layout (the env's default there)
+def test_advanced_env_matches_oracle_composition(device, N):
     import torch
 
     from gymca_amd.forest_fire.bulldozer import AdvancedForestFireBulldozerEnv
     from oracle.windy import move
 
-    E, N = 4, 64
+    E = 4
     env = AdvancedForestFireBulldozerEnv(N, N, key=99, num_envs=E, use_hidden=True, device=device)
+    assert env.slope_layout == ("packed" if N == 256 else "edge")
     env.reset()
     case = make_case(E, N, N, 44)
     env.set_state(grid=case["grid"], fire_age=case["age"], vegetation=np.clip(case["veg"], 1, 5),
