@@ -294,6 +294,22 @@ def bench_windy(args, world, rank, device, pg):
             env.ca_step_all()
 
     dt_ca, kern = timed_loop(ca_step, K, args.warmup, pg, device)
+    # the same-size ceiling: a device copy of the CA's bytes (E x H x W in, the same out) on this GPU
+    src = torch.empty(E * N * N, dtype=torch.uint8, device=device)
+    dst = torch.empty_like(src)
+
+    def copy_step(events):
+        if events is not None:
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            dst.copy_(src)
+            b.record()
+            events.append((a, b))
+        else:
+            dst.copy_(src)
+
+    _, kern_copy = timed_loop(copy_step, K, args.warmup, pg, device)
+    del src, dst
     return {
         "config": "ForestFireBulldozer 256x256, 1024 envs/GPU, WindyForestFire",
         "env_steps_per_s": world * E * Kg * G / dt_env,
@@ -303,6 +319,8 @@ def bench_windy(args, world, rank, device, pg):
         "ca_kernel_ms": kern * 1e3,
         "ca_achieved_gbs": WINDY_BYTES_PER_CELL * E * N * N / kern / 1e9,
         "ca_roofline_frac": WINDY_BYTES_PER_CELL * E * N * N / kern / 1e9 / HBM_PEAK_GBS,
+        "same_size_copy_ms": kern_copy * 1e3,
+        "ca_frac_of_same_size_copy": kern_copy / kern,
     }
 
 

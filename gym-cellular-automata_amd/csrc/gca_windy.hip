@@ -254,7 +254,11 @@ static void launch_fast(uint8_t* b0, uint8_t* b1, const uint8_t* parity, const i
     constexpr int RPW = 64 / LPR;
     // strip height: >= 32 rows when there is enough work, multiple of RPW
     const int64_t rows = (int64_t)E * H;
+#ifdef GCA_WINDY_SH
+    int SH = GCA_WINDY_SH;  // A/B hook (scripts/build_variant.sh)
+#else
     int SH = 32;
+#endif
     while (SH > RPW && rows / SH < 8192) SH >>= 1;
     if (SH < RPW) SH = RPW;
     SH = ((SH + RPW - 1) / RPW) * RPW;
