@@ -135,6 +135,37 @@ __global__ __launch_bounds__(256) void alex_es_pattern_k(const uint8_t* __restri
     *(uint4*)(ao + off + 8) = a1;
 }
 
+// wave-sequential static layout: each wave's 1024 cells keep their static bytes (4 slope planes x 4 B + vd 1 B
+// = 17 B/cell) in one contiguous 17 KiB block read front to back, 1 KiB per load instruction; the row r+1 slope
+// planes (12 B/cell) come from the next wave's block (cache hits); dynamic grid u8 + age i16 read and written.
+__global__ __launch_bounds__(256) void alex_wave_pattern_k(const uint8_t* __restrict__ g, uint8_t* __restrict__ go,
+                                                           const int16_t* __restrict__ a, int16_t* __restrict__ ao,
+                                                           const float4* __restrict__ st, int nwaves) {
+    const int lane = threadIdx.x & 63;
+    const int wv = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const size_t off = (size_t)wv * 1024 + lane * 16;
+    const uint4 g4 = *(const uint4*)(g + off);
+    const uint4 a0 = *(const uint4*)(a + off);
+    const uint4 a1 = *(const uint4*)(a + off + 8);
+    const float4* blk = st + (size_t)wv * 1088;  // 17 KiB = 1088 float4
+    const float4* nxt = st + (size_t)min(wv + 1, nwaves - 1) * 1088;
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 17; ++i) {
+        const float4 v = blk[i * 64 + lane];
+        acc += v.x + v.y + v.z + v.w;
+    }
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+        const float4 v = nxt[i * 64 + lane];
+        acc += v.x + v.y + v.z + v.w;
+    }
+    const uint32_t mix = (acc > 1e30f) ? 1u : 0u;
+    *(uint4*)(go + off) = make_uint4(g4.x ^ mix, g4.y, g4.z, g4.w);
+    *(uint4*)(ao + off) = make_uint4(a0.x, a0.y ^ mix, a0.z, a0.w);
+    *(uint4*)(ao + off + 8) = a1;
+}
+
 #define TIME10(launch, out_ms) do { launch; CK(hipEventRecord(e0)); for (int i_ = 0; i_ < 10; ++i_) { launch; } \
     CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1)); CK(hipEventElapsedTime(&out_ms, e0, e1)); out_ms /= 10; } while (0)
 
@@ -189,6 +220,15 @@ int main() {
     TIME10((alex_es_pattern_k<0><<<nblk, 256>>>(g, go, a, ao, v, d, du, ps, HW, 256)), ms);
     printf("\"es_pattern_lane64_ms\": %.4f, \"es_pattern_lane64_gbs\": %.1f, ", ms, 25.0 * cells / (ms * 1e-3) / 1e9);
     TIME10((alex_es_pattern_k<1><<<nblk, 256>>>(g, go, a, ao, v, d, du, ps, HW, 256)), ms);
-    printf("\"es_pattern_coal_ms\": %.4f, \"es_pattern_coal_gbs\": %.1f}\n", ms, 25.0 * cells / (ms * 1e-3) / 1e9);
+    printf("\"es_pattern_coal_ms\": %.4f, \"es_pattern_coal_gbs\": %.1f, ", ms, 25.0 * cells / (ms * 1e-3) / 1e9);
+    // the same access pattern at the step kernel's occupancy: 36 KB of (unused) LDS per block -> 4 blocks / CU
+    TIME10((alex_es_pattern_k<1><<<nblk, 256, 36864>>>(g, go, a, ao, v, d, du, ps, HW, 256)), ms);
+    printf("\"es_pattern_coal_occ4_ms\": %.4f, ", ms);
+    TIME10((alex_es_pattern_k<1><<<nblk, 256, 27648>>>(g, go, a, ao, v, d, du, ps, HW, 256)), ms);
+    printf("\"es_pattern_coal_occ5_ms\": %.4f, ", ms);
+    TIME10((alex_es_pattern_k<1><<<nblk, 256, 18432>>>(g, go, a, ao, v, d, du, ps, HW, 256)), ms);
+    printf("\"es_pattern_coal_occ8_ms\": %.4f, ", ms);
+    TIME10((alex_wave_pattern_k<<<nblk, 256>>>(g, go, a, ao, reinterpret_cast<const float4*>(ps), nblk * 4)), ms);
+    printf("\"wave_seq_pattern_ms\": %.4f, \"wave_seq_pattern_gbs\": %.1f}\n", ms, 23.0 * cells / (ms * 1e-3) / 1e9);
     return 0;
 }
