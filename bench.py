@@ -50,6 +50,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--slope-layout", choices=["packed", "edge", "planes"], default="packed")
+    ap.add_argument("--tile-skip", action="store_true", help="A/B: headline with the tile activity map on")
     ap.add_argument("--headline-only", action="store_true",
                     help="only the headline loop (no RGB / episode-start loops): every alex_step launch is the "
                          "dense mid-episode one, so rocprofv3 per-kernel averages match kernel_ms")
@@ -129,7 +130,7 @@ def bench_alex(args, world, rank, device, pg):
     E, N = args.envs, args.size
     env = AdvancedForestFireBulldozerEnv(N, N, key=1, num_envs=E, use_hidden=False, device=device,
                                          env_offset=rank * E, slope_layout=args.slope_layout, observation="rgb",
-                                         enable_extensions=True)
+                                         enable_extensions=True, tile_skip=args.tile_skip)
     env.reset()
     synthetic_state(env, rank, device)
     action = torch.zeros((E, 2), dtype=torch.int32, device=device)
@@ -194,6 +195,13 @@ def bench_alex(args, world, rank, device, pg):
     dt_sp, kern_sp = timed_loop(step, args.steps, args.warmup, pg, device)
     res["episode_start"] = {"cell_updates_per_s": world * E * N * N * args.steps / dt_sp,
                             "kernel_ms": kern_sp * 1e3, "state": "reset state (2 fires per env), fire-sparsity skip"}
+    # the same episode start with the opt-in tile activity map (tiles without fire nearby copied, not stepped)
+    env.set_tile_skip(True)
+    env.reset()
+    dt_ts, kern_ts = timed_loop(step, args.steps, args.warmup, pg, device)
+    res["episode_start"]["tile_skip"] = {"cell_updates_per_s": world * E * N * N * args.steps / dt_ts,
+                                         "kernel_ms": kern_ts * 1e3}
+    env.set_tile_skip(args.tile_skip)
     return res
 
 

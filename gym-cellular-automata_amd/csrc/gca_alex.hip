@@ -144,7 +144,8 @@ __global__ __launch_bounds__(256, GCA_ALEX_WGS) void alex_step_kernel(
     const uint8_t* __restrict__ veg, const uint8_t* __restrict__ den, const uint8_t* __restrict__ dousing,
     const float* __restrict__ p_slope, const int32_t* __restrict__ wind_index, const uint32_t* __restrict__ rng_step,
     const float* __restrict__ inj_burn, const float* __restrict__ inj_grow, const int32_t* __restrict__ inj_age,
-    float* __restrict__ prob_out, int32_t* __restrict__ counts) {
+    float* __restrict__ prob_out, int32_t* __restrict__ counts, const uint8_t* __restrict__ act_in,
+    uint8_t* __restrict__ act_out) {
     constexpr bool INJECT = MODE == 2;
     constexpr bool PROB = MODE != 0;
     constexpr int RS = R < 2 ? 2 : R;  // staged halo: heat radius, at least the 5x5 dousing box
@@ -324,6 +325,57 @@ __global__ __launch_bounds__(256, GCA_ALEX_WGS) void alex_step_kernel(
                 }
             }
         }
+    }
+    // ---- tile activity map (PK, the env's path; act_in only with p_tree == 0, checked on the host): a tile with
+    //      no FIRE in itself or its 8 neighbour tiles at the step's input cannot change — no tree has a burning
+    //      neighbour, no fire ages, nothing grows — so it is copied instead of stepped: the grid (own cells, loaded
+    //      above), and the ages only when they are not updated in place (the env's ages are). Checked here, after
+    //      the staging loads are issued, so the flags' latency hides under them. act_out[tile] = any FIRE in the
+    //      step's output tile: 0 here, set to 1 below by every wave that leaves a FIRE (ordered after this store
+    //      by the workgroup barrier).
+    if (PK && act_out) {
+        const int tiles_all = tiles_r * tiles_c;
+        if (act_in) {
+            const int ti = tile / tiles_c, tj = tile - ti * tiles_c;
+            const uint8_t* A = act_in + (size_t)e * tiles_all;
+            int anyf = 0;
+#pragma unroll
+            for (int di = -1; di <= 1; ++di)
+#pragma unroll
+                for (int dj = -1; dj <= 1; ++dj) {
+                    const int a = ti + di, b = tj + dj;
+                    if (a >= 0 && a < tiles_r && b >= 0 && b < tiles_c) anyf |= A[a * tiles_c + b];
+                }
+            if (!anyf) {
+                *reinterpret_cast<uint4*>(grid_out + (size_t)e * HW + lo) = make_uint4(own[0], own[1], own[2], own[3]);
+                if (age_in != age_out) {
+                    const uint4 a0 = *reinterpret_cast<const uint4*>(age_in + (size_t)e * HW + lo);
+                    const uint4 a1 = *reinterpret_cast<const uint4*>(age_in + (size_t)e * HW + lo + 8);
+                    *reinterpret_cast<uint4*>(age_out + (size_t)e * HW + lo) = a0;
+                    *reinterpret_cast<uint4*>(age_out + (size_t)e * HW + lo + 8) = a1;
+                }
+                if (tid == 0) act_out[(size_t)e * tiles_all + tile] = 0;
+                if (counts) {
+                    int cE = 0, cT = 0;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        cE += __builtin_popcount(bytes_eq01(own[j], Ep));
+                        cT += __builtin_popcount(bytes_eq01(own[j], Tp));
+                    }
+#pragma unroll
+                    for (int off = 32; off > 0; off >>= 1) {
+                        cE += __shfl_xor(cE, off);
+                        cT += __shfl_xor(cT, off);
+                    }
+                    if ((tid & 63) == 0) {
+                        if (cE) atomicAdd(counts + 3 * e + 0, cE);
+                        if (cT) atomicAdd(counts + 3 * e + 1, cT);
+                    }
+                }
+                return;  // the whole workgroup (anyf is workgroup-uniform)
+            }
+        }
+        if (tid == 0) act_out[(size_t)e * tiles_all + tile] = 0;
     }
     int near_fire = 0;  // a FIRE cell within one row of the tile (rows r0-1 .. r0+TH) in this thread's chunks
 #pragma unroll
@@ -783,7 +835,7 @@ __global__ __launch_bounds__(256, GCA_ALEX_WGS) void alex_step_kernel(
             }
         }
     }
-    if (counts) {
+    if (counts || (PK && act_out)) {
         int cntT = __builtin_popcount(newT & okB), cntF = __builtin_popcount(newF & okB),
             cntE = __builtin_popcount(newE & okB);
 #pragma unroll
@@ -793,9 +845,12 @@ __global__ __launch_bounds__(256, GCA_ALEX_WGS) void alex_step_kernel(
             cntE += __shfl_xor(cntE, off);
         }
         if ((tid & 63) == 0) {
-            if (cntE) atomicAdd(counts + 3 * e + 0, cntE);
-            if (cntT) atomicAdd(counts + 3 * e + 1, cntT);
-            if (cntF) atomicAdd(counts + 3 * e + 2, cntF);
+            if (counts) {
+                if (cntE) atomicAdd(counts + 3 * e + 0, cntE);
+                if (cntT) atomicAdd(counts + 3 * e + 1, cntT);
+                if (cntF) atomicAdd(counts + 3 * e + 2, cntF);
+            }
+            if (PK && act_out && cntF) act_out[(size_t)e * tiles_r * tiles_c + tile] = 1;
         }
     }
 }
@@ -819,7 +874,7 @@ template <int R, int MODE, bool ES, bool PK = false>
 void launch_alex(const gca_alex_params& p, int E, int H, int W, const uint8_t* gi, uint8_t* go, const int16_t* ai,
                  int16_t* ao, const uint8_t* veg, const uint8_t* den, const uint8_t* dous, const float* ps,
                  const int32_t* wi, const uint32_t* rs, const float* ib, const float* ig, const int32_t* ia, float* po,
-                 int32_t* counts, hipStream_t st) {
+                 int32_t* counts, hipStream_t st, const uint8_t* act_in = nullptr, uint8_t* act_out = nullptr) {
     const int tiles_r = (H + TH - 1) / TH, tiles_c = (W + TW - 1) / TW;
     constexpr int RS = R < 2 ? 2 : R;
     constexpr int RR = TH + 2 * RS;
@@ -830,22 +885,22 @@ void launch_alex(const gca_alex_params& p, int E, int H, int W, const uint8_t* g
                         ((uintptr_t)den) | ((uintptr_t)dous) | ((uintptr_t)ps)) & 15u) == 0;
     if (PK)  // packed env layout (the host checked the FAST shape and alignment)
         hipLaunchKernelGGL((alex_step_kernel<R, 0, true, true, true>), grid, dim3(256), lds, st, p, H, W, tiles_r,
-                           tiles_c, gi, go, ai, ao, veg, den, dous, ps, wi, rs, ib, ig, ia, po, counts);
+                           tiles_c, gi, go, ai, ao, veg, den, dous, ps, wi, rs, ib, ig, ia, po, counts, act_in, act_out);
     else if (fast)  // production shape: no per-lane bounds checks (instantiated for the Philox mode only)
         hipLaunchKernelGGL((alex_step_kernel<R, MODE, MODE == 0, ES>), grid, dim3(256), lds, st, p, H, W, tiles_r,
-                           tiles_c, gi, go, ai, ao, veg, den, dous, ps, wi, rs, ib, ig, ia, po, counts);
+                           tiles_c, gi, go, ai, ao, veg, den, dous, ps, wi, rs, ib, ig, ia, po, counts, act_in, act_out);
     else
         hipLaunchKernelGGL((alex_step_kernel<R, MODE, false, ES>), grid, dim3(256), lds, st, p, H, W, tiles_r, tiles_c,
-                           gi, go, ai, ao, veg, den, dous, ps, wi, rs, ib, ig, ia, po, counts);
+                           gi, go, ai, ao, veg, den, dous, ps, wi, rs, ib, ig, ia, po, counts, act_in, act_out);
 }
 
 template <int MODE, bool ES, bool PK = false>
 void dispatch_r(int R, const gca_alex_params& p, int E, int H, int W, const uint8_t* gi, uint8_t* go, const int16_t* ai,
                 int16_t* ao, const uint8_t* veg, const uint8_t* den, const uint8_t* dous, const float* ps,
                 const int32_t* wi, const uint32_t* rs, const float* ib, const float* ig, const int32_t* ia, float* po,
-                int32_t* counts, hipStream_t st) {
+                int32_t* counts, hipStream_t st, const uint8_t* act_in = nullptr, uint8_t* act_out = nullptr) {
 #define GCA_ALEX_CASE(RV) \
-    case RV: launch_alex<RV, MODE, ES, PK>(p, E, H, W, gi, go, ai, ao, veg, den, dous, ps, wi, rs, ib, ig, ia, po, counts, st); break;
+    case RV: launch_alex<RV, MODE, ES, PK>(p, E, H, W, gi, go, ai, ao, veg, den, dous, ps, wi, rs, ib, ig, ia, po, counts, st, act_in, act_out); break;
     switch (R) {
         GCA_ALEX_CASE(1) GCA_ALEX_CASE(2) GCA_ALEX_CASE(3) GCA_ALEX_CASE(4)
         GCA_ALEX_CASE(5) GCA_ALEX_CASE(6) GCA_ALEX_CASE(7) GCA_ALEX_CASE(8)
@@ -885,13 +940,13 @@ static int alex_step_impl(bool es, const gca_alex_params* p, int E, int H, int W
     }
     if (inj)
         (es ? dispatch_r<2, true> : dispatch_r<2, false>)(p->R, *p, E, H, W, grid_in, grid_out, age_in, age_out, veg, den, dousing, p_slope, wind_index,
-                         rng_step, inj_burn, inj_grow, inj_age, prob_out, counts, st);
+                         rng_step, inj_burn, inj_grow, inj_age, prob_out, counts, st, nullptr, nullptr);
     else if (prob_out)
         (es ? dispatch_r<1, true> : dispatch_r<1, false>)(p->R, *p, E, H, W, grid_in, grid_out, age_in, age_out, veg, den, dousing, p_slope, wind_index,
-                      rng_step, nullptr, nullptr, nullptr, prob_out, counts, st);
+                      rng_step, nullptr, nullptr, nullptr, prob_out, counts, st, nullptr, nullptr);
     else
         (es ? dispatch_r<0, true> : dispatch_r<0, false>)(p->R, *p, E, H, W, grid_in, grid_out, age_in, age_out, veg, den, dousing, p_slope, wind_index,
-                      rng_step, nullptr, nullptr, nullptr, nullptr, counts, st);
+                      rng_step, nullptr, nullptr, nullptr, nullptr, counts, st, nullptr, nullptr);
     GCA_CHECK_LAUNCH(es ? "alex_step_es" : "alex_step");
     return GCA_OK;
 }
@@ -918,14 +973,16 @@ extern "C" int gca_alex_step_es(const gca_alex_params* p, int E, int H, int W, c
 extern "C" int gca_alex_step_packed(const gca_alex_params* p, int E, int H, int W, const uint8_t* grid_in,
                                     uint8_t* grid_out, const int16_t* age_in, int16_t* age_out, const uint8_t* vd,
                                     const uint16_t* dous_bits, const float* edge_slope_coal, const int32_t* wind_index,
-                                    const uint32_t* rng_step, int32_t* counts, void* stream) {
+                                    const uint32_t* rng_step, int32_t* counts, const uint8_t* act_in, uint8_t* act_out,
+                                    void* stream) {
     GCA_CHECK_ARG(p && grid_in && grid_out && age_in && age_out && vd && dous_bits && edge_slope_coal && wind_index,
                   "alex_step_packed: null argument");
     GCA_CHECK_ARG(E > 0 && H > 0 && W > 0 && W % TW == 0 && H % TH == 0,
                   "alex_step_packed: W must be a multiple of 256 and H of 16");
     GCA_CHECK_ARG(p->R >= 1 && p->R <= GCA_MAX_RADIUS, "alex_step_packed: burn radius must be in [1, 8]");
     GCA_CHECK_ARG(p->n_winds >= 1 && p->n_winds <= 16, "alex_step_packed: 1..16 wind matrices");
-    GCA_CHECK_ARG(grid_in != grid_out && age_in != age_out, "alex_step_packed: in-place update is not supported");
+    // ages may be updated in place (each lane reads and writes only its own cells); the grid may not (halos)
+    GCA_CHECK_ARG(grid_in != grid_out, "alex_step_packed: the grid cannot be updated in place");
     GCA_CHECK_ARG(((((uintptr_t)grid_in) | ((uintptr_t)grid_out) | ((uintptr_t)age_in) | ((uintptr_t)age_out) |
                     ((uintptr_t)vd) | ((uintptr_t)edge_slope_coal)) & 15u) == 0 && ((uintptr_t)dous_bits & 1u) == 0,
                   "alex_step_packed: arrays must be 16-B aligned");
@@ -934,9 +991,13 @@ extern "C" int gca_alex_step_packed(const gca_alex_params* p, int E, int H, int 
         gca_set_error("alex_step_packed: counts memset failed");
         return GCA_ERR_HIP;
     }
+    GCA_CHECK_ARG(!act_in || act_out, "alex_step_packed: act_in needs act_out");
+    GCA_CHECK_ARG(act_in != act_out || !act_in, "alex_step_packed: act_in and act_out must differ");
+    // a tile without fire nearby can still change when EMPTY cells grow: the skip needs p_tree == 0
+    const uint8_t* ain = (p->p_tree > 0.0f) ? nullptr : act_in;
     dispatch_r<0, true, true>(p->R, *p, E, H, W, grid_in, grid_out, age_in, age_out, vd, nullptr,
                               reinterpret_cast<const uint8_t*>(dous_bits), edge_slope_coal, wind_index, rng_step, nullptr,
-                              nullptr, nullptr, nullptr, counts, st);
+                              nullptr, nullptr, nullptr, counts, st, ain, act_out);
     GCA_CHECK_LAUNCH("alex_step_packed");
     return GCA_OK;
 }

@@ -39,8 +39,8 @@ __global__ __launch_bounds__(256) void alex_pinecones_kernel(gca_pine_params p, 
                                                              const int32_t* __restrict__ wind_index,
                                                              const uint32_t* __restrict__ s_cdf,
                                                              const uint32_t* __restrict__ rng_step,
-                                                             int32_t* __restrict__ counts, int64_t chunks_per_env,
-                                                             int E) {
+                                                             int32_t* __restrict__ counts, uint8_t* __restrict__ act,
+                                                             int64_t chunks_per_env, int E) {
     const int64_t gch = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int e = (int)(gch / chunks_per_env);
     if (e >= E) return;
@@ -99,6 +99,10 @@ __global__ __launch_bounds__(256) void alex_pinecones_kernel(gca_pine_params p, 
                     atomicSub(counts + 3 * e + 1, 1);
                     atomicAdd(counts + 3 * e + 2, 1);
                 }
+                if (act) {  // the step's tile activity map (16 x 256 tiles): the target's tile now burns
+                    const int tcw = (W + 255) / 256, tch = (H + 15) / 16;
+                    act[(int64_t)e * tch * tcw + (tr / 16) * tcw + tc / 256] = 1;
+                }
             }
         }
     }
@@ -109,7 +113,7 @@ __global__ __launch_bounds__(256) void alex_pinecones_kernel(gca_pine_params p, 
 extern "C" int gca_alex_pinecones(const gca_pine_params* p, int E, int H, int W, const uint8_t* grid_in,
                                   uint8_t* grid_out, int16_t* age_out, const uint8_t* veg, const uint8_t* den,
                                   const int32_t* wind_index, const uint32_t* s_cdf, const uint32_t* rng_step,
-                                  int32_t* counts, void* stream) {
+                                  int32_t* counts, uint8_t* act_tiles, void* stream) {
     GCA_CHECK_ARG(p && grid_in && grid_out && age_out && veg && den && wind_index && s_cdf,
                   "alex_pinecones: null argument");
     GCA_CHECK_ARG(E > 0 && H > 0 && W > 0 && grid_in != grid_out, "alex_pinecones: bad sizes or aliased grids");
@@ -119,7 +123,7 @@ extern "C" int gca_alex_pinecones(const gca_pine_params* p, int E, int H, int W,
     const int64_t cpe = ((int64_t)H * W + 15) / 16;
     const int64_t n = cpe * E;
     hipLaunchKernelGGL(alex_pinecones_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *p,
-                       H, W, grid_in, grid_out, age_out, veg, den, wind_index, s_cdf, rng_step, counts, cpe, E);
+                       H, W, grid_in, grid_out, age_out, veg, den, wind_index, s_cdf, rng_step, counts, act_tiles, cpe, E);
     GCA_CHECK_LAUNCH("alex_pinecones");
     return GCA_OK;
 }

@@ -162,8 +162,8 @@ _SIGNATURES = {
     "gca_alex_step_es": ([POINTER(AlexParams), c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
                          c_int),
     "gca_alex_edge_slope_from_altitude": ([P, P, c_int, c_int, c_int, P], c_int),
-    "gca_alex_pinecones": ([POINTER(PineParams), c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P], c_int),
-    "gca_alex_step_packed": ([POINTER(AlexParams), c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, P], c_int),
+    "gca_alex_pinecones": ([POINTER(PineParams), c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, P], c_int),
+    "gca_alex_step_packed": ([POINTER(AlexParams), c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, P, P, P], c_int),
     "gca_alex_pack_layers": ([P, P, P, P, P, c_int, c_int, c_int, P], c_int),
     "gca_alex_edge_slope_coalesce": ([P, P, c_int, c_int, c_int, P], c_int),
     "gca_alex_edge_factors": ([P, P, P, c_int64, P], c_int),

@@ -38,7 +38,7 @@ class AdvancedForestFireBulldozerEnv:
     def __init__(self, nrows, ncols, key=0, num_envs=8, speed_move=0.12, speed_act=0.03, speed_multiplier=1.0,
                  pos_bull=None, pos_fire=None, t_move=None, t_shoot=None, t_any=0.001, p_tree=0.90, p_empty=0.10,
                  use_hidden=True, middle_fire=False, enable_extensions=False, device=None, env_offset=0,
-                 hidden_rng=None, slope_layout="auto", observation="grid", pinecones=False):
+                 hidden_rng=None, slope_layout="auto", observation="grid", pinecones=False, tile_skip=False):
         import torch
 
         self.device = dev.require_device(device)
@@ -97,12 +97,19 @@ class AdvancedForestFireBulldozerEnv:
         if slope_layout == "packed" and (W % 256 or H % 16):
             raise ValueError("slope_layout='packed' needs W % 256 == 0 and H % 16 == 0")
         self.slope_layout = slope_layout
+        if slope_layout == "packed":  # the packed step updates ages in place: both "buffers" are one (stride 0)
+            self.age = torch.zeros((E, H, W), dtype=torch.int16, **kw).unsqueeze(0).expand(2, E, H, W)
         # edge: (E, 4, H, W) edge values for gca_alex_step_es (packed: the same in coalesced order);
         # planes: (E, 8, H, W) p_slope for gca_alex_step
         self.slope_data = torch.zeros((E, 8 if slope_layout == "planes" else 4, H, W), dtype=torch.float32, **kw)
         # packed layout extras: vd = min(veg, 7) | min(den, 7) << 4 and the dousing bits (u16 per 16 columns)
         self.vd = torch.zeros((E, H, W), dtype=torch.uint8, **kw) if slope_layout == "packed" else None
         self.dous_bits = torch.zeros((E, H * W // 16), dtype=torch.int16, **kw) if slope_layout == "packed" else None
+        # tile activity map of the packed step (16 x 256 tiles; ping-pong with the grid): tiles whose 3 x 3 tile
+        # neighbourhood holds no fire are copied instead of stepped (exact: p_tree = 0 here); all ones = unknown.
+        # Opt-in: it makes a sparse state's step ~20% faster and a dense one ~3% slower
+        self.act = None
+        self.set_tile_skip(tile_skip)
         self.wind_index = torch.zeros(E, dtype=torch.int32, **kw)
         self.pine_tables = (torch.as_tensor(s_cdf_tables(self._winds).view(np.int32), **kw) if self.pinecones
                             else None)
@@ -149,6 +156,16 @@ class AdvancedForestFireBulldozerEnv:
             self.vegetation.fill_(3)
         self._slopes_from(self.altitude)
         self._pack_layers()
+
+    def set_tile_skip(self, on):
+        """Switch the packed step's tile activity map on / off (the map restarts as "every tile active")."""
+        import torch
+
+        E, H, W = self.num_envs, self.nrows, self.ncols
+        if on and self.slope_layout != "packed":
+            raise ValueError("tile skipping needs the packed layout (W % 256 == 0, H % 16 == 0)")
+        self.act = (torch.ones((2, E, (H // 16) * (W // 256)), dtype=torch.uint8, device=self.device) if on
+                    else None)
 
     def _pack_layers(self):
         """vd and dousing bits of the packed layout from the u8 layers (no-op for the other layouts)."""
@@ -218,6 +235,8 @@ class AdvancedForestFireBulldozerEnv:
         self.dousing.zero_()
         if self.dous_bits is not None:
             self.dous_bits.zero_()
+        if self.act is not None:
+            self.act.fill_(1)
         self.accu.zero_()
         self.time_step.fill_(1)
         self.is_night.zero_()
@@ -270,6 +289,8 @@ class AdvancedForestFireBulldozerEnv:
             self._slopes_from(self.altitude)
         if vegetation is not None or density is not None or dousing is not None:
             self._pack_layers()
+        if self.act is not None:  # the state may have fire anywhere now
+            self.act.fill_(1)
         call("gca_count_cells", dev.ptr(self.grid[self.cur]), E, H, W, self._empty, self._tree, self._fire,
              dev.ptr(self.counts), st)
 
@@ -305,6 +326,7 @@ class AdvancedForestFireBulldozerEnv:
             call("gca_alex_step_packed", self.alex_params, E, H, W, dev.ptr(self.grid[a]), dev.ptr(self.grid[b]),
                  dev.ptr(self.age[a]), dev.ptr(self.age[b]), dev.ptr(self.vd), dev.ptr(self.dous_bits),
                  dev.ptr(self.slope_data), dev.ptr(self.wind_index), dev.ptr(self.rng_step), dev.ptr(self.counts),
+                 dev.ptr(None if self.act is None else self.act[a]), dev.ptr(None if self.act is None else self.act[b]),
                  dev.stream_ptr(self.device))
             self._pinecones(a, b)
             self.cur = b
@@ -322,7 +344,8 @@ class AdvancedForestFireBulldozerEnv:
             E, H, W = self.num_envs, self.nrows, self.ncols
             call("gca_alex_pinecones", self.pine_params, E, H, W, dev.ptr(self.grid[a]), dev.ptr(self.grid[b]),
                  dev.ptr(self.age[b]), dev.ptr(self.vegetation), dev.ptr(self.density), dev.ptr(self.wind_index),
-                 dev.ptr(self.pine_tables), dev.ptr(self.rng_step), dev.ptr(self.counts), dev.stream_ptr(self.device))
+                 dev.ptr(self.pine_tables), dev.ptr(self.rng_step), dev.ptr(self.counts),
+                 dev.ptr(None if self.act is None else self.act[b]), dev.stream_ptr(self.device))
 
     def step(self, action):
         """action: (E, 2) or (E, 3) ints (move, shoot[, extension]); device tensor or numpy."""
@@ -362,6 +385,8 @@ class AdvancedForestFireBulldozerEnv:
         self.steps_elapsed.masked_fill_(mask, 0)
         self.reward_accumulated.masked_fill_(mask, 0.0)
         self.rng_step.masked_fill_(mask, 0)  # the reference re-injects the initial JAX key
+        if self.act is not None:  # re-injected envs: their fire is back, every tile active
+            self.act[self.cur].masked_fill_(mask[:, None], 1)
         self.counts.copy_(torch.where(mask[:, None], init["counts"], self.counts))
         t, f = self.counts[:, 1].float(), self.counts[:, 2].float()
         self.reward.copy_(torch.where(mask, -(f / (t + f + 1e-8)), self.reward))

@@ -198,7 +198,7 @@ class PartiallyObservableForestFireJax(Operator):
             pp = make_pine_params(seed, self.empty, self.tree, self.fire)
             tabs = torch.as_tensor(s_cdf_tables(shared_context["winds"]).view(np.int32), device=device)
             call("gca_alex_pinecones", pp, E, H, W, dev.ptr(grid_in), dev.ptr(grid_out), dev.ptr(age_out),
-                 dev.ptr(veg), dev.ptr(den), dev.ptr(widx), dev.ptr(tabs), dev.ptr(rng_step), None, st)
+                 dev.ptr(veg), dev.ptr(den), dev.ptr(widx), dev.ptr(tabs), dev.ptr(rng_step), None, None, st)
         new_widx = widx.clone()
         call("gca_alex_wind_change", float(np.float32(shared_context.get("p_wind_change", 0.06))), p.n_winds,
              p.seed, 0, dev.ptr(rng_step), dev.ptr(wu), dev.ptr(wk), dev.ptr(new_widx), E, st)

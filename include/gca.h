@@ -170,11 +170,15 @@ int gca_alex_step_es(const gca_alex_params* p, int E, int H, int W, const uint8_
  * arrays): vd[e][r][c] = min(veg, 7) | min(den, 7) << 4; dous_bits[e][r][c / 16] bit c % 16 = (dousing != 0)
  * (the env's dousing counts are 0/1: ModifyJax writes 1, move_modify_jax.py:102-114); edge_slope_coal = the edge
  * layout with every 256-column row segment of a plane in coalesced order (gca_alex_edge_slope_coalesce).
- * Results are bit-identical to gca_alex_step_es on the unpacked arrays. Same replaced code as gca_alex_step. */
+ * Results are bit-identical to gca_alex_step_es on the unpacked arrays. Same replaced code as gca_alex_step.
+ * Tile activity map (nullable): act_out[e][tile] (u8, tiles of 16 rows x 256 columns, row-major) receives 1 iff
+ * the step leaves a FIRE in that tile; with act_in = the previous step's act_out (or all ones), a tile whose 3 x 3
+ * tile neighbourhood has no fire is copied instead of stepped (exact when p_tree == 0: act_in is ignored
+ * otherwise). act_out is required with act_in; act_out alone just records the map. */
 int gca_alex_step_packed(const gca_alex_params* p, int E, int H, int W, const uint8_t* grid_in, uint8_t* grid_out,
                          const int16_t* age_in, int16_t* age_out, const uint8_t* vd, const uint16_t* dous_bits,
                          const float* edge_slope_coal, const int32_t* wind_index, const uint32_t* rng_step,
-                         int32_t* counts, void* stream);
+                         int32_t* counts, const uint8_t* act_in, uint8_t* act_out, void* stream);
 /* vd (nullable) and dous_bits of gca_alex_step_packed from veg / den / dousing (E,H,W) u8; W % 16 == 0. */
 int gca_alex_pack_layers(const uint8_t* veg, const uint8_t* den, const uint8_t* dousing, uint8_t* vd,
                          uint16_t* dous_bits, int E, int H, int W, void* stream);
@@ -226,7 +230,8 @@ int gca_alex_altitude_apply(double* altitude, int E, int H, int W, const int32_t
  * randint(age_lo, age_hi) and one count moves tree -> fire. Any burning pinecone ignites its target
  * (duplicates). s_cdf [n_winds][8][GCA_PINE_CDF] u32: per (wind, direction) t[0] = 2K, t[1..2K] = 32-bit
  * thresholds of P(s <= -K + j) (gymca_amd/forest_fire/operators/pinecones.py). Draws: Philox blocks
- * (lin, env, step, PINE + 0 / 1 + m) and (target lin, env, step, PINA), see gca_pine.hip.            */
+ * (lin, env, step, PINE + 0 / 1 + m) and (target lin, env, step, PINA), see gca_pine.hip. act_tiles
+ * (nullable): gca_alex_step_packed's act_out of the same step — the tile of every ignited target is set to 1. */
 #define GCA_PINE_MAX 8
 #define GCA_PINE_CDF 17
 typedef struct {
@@ -242,7 +247,7 @@ typedef struct {
 } gca_pine_params;
 int gca_alex_pinecones(const gca_pine_params* p, int E, int H, int W, const uint8_t* grid_in, uint8_t* grid_out,
                        int16_t* age_out, const uint8_t* veg, const uint8_t* den, const int32_t* wind_index,
-                       const uint32_t* s_cdf, const uint32_t* rng_step, int32_t* counts, void* stream);
+                       const uint32_t* s_cdf, const uint32_t* rng_step, int32_t* counts, uint8_t* act_tiles, void* stream);
 
 /* --------------------------------- AdvancedForestFireBulldozer env step (batched)
  * advanced_bulldozer.py:1103-1133 minus observations, + _award/_is_done :597-633.  */

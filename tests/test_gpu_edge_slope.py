@@ -229,7 +229,7 @@ def packed_step(device, p, case, es, rng_step):
     go, ao = torch.empty_like(g), torch.empty_like(a)
     counts = torch.zeros((E, 3), dtype=torch.int32, device=device)
     call("gca_alex_step_packed", p, E, H, W, dev.ptr(g), dev.ptr(go), dev.ptr(a), dev.ptr(ao), dev.ptr(vd),
-         dev.ptr(bits), dev.ptr(coal), dev.ptr(wi), dev.ptr(rs), dev.ptr(counts), dev.stream_ptr())
+         dev.ptr(bits), dev.ptr(coal), dev.ptr(wi), dev.ptr(rs), dev.ptr(counts), None, None, dev.stream_ptr())
     return go.cpu().numpy(), ao.cpu().numpy(), counts.cpu().numpy(), coal.cpu().numpy(), bits.cpu().numpy()
 
 
@@ -286,3 +286,41 @@ def test_env_packed_and_edge_layouts_agree(device):
                 env.done[1] = 1
                 env.conditional_reset()
     assert int(envs[0].dousing.sum()) > 0
+
+
+@pytest.mark.parametrize("pinecones", [False, True])
+def test_tile_skip_matches_full_step(device, pinecones):
+    """The packed step's tile activity map (tiles with no fire in their 3 x 3 tile neighbourhood are copied,
+    not stepped) changes nothing: env trajectories from the reset state (two fires per env: most tiles skip)
+    and from a mid-episode state equal the same env with tile_skip=False, grid, ages, rewards and done, over
+    steps with shooting, pinecones (which ignite tiles far from the fire front) and a conditional reset."""
+    from gymca_amd.forest_fire.bulldozer import AdvancedForestFireBulldozerEnv
+
+    E, N = 3, 256
+    envs = [AdvancedForestFireBulldozerEnv(N, N, key=21, num_envs=E, use_hidden=True, device=device,
+                                           hidden_rng=np.random.RandomState(4), pinecones=pinecones, tile_skip=ts)
+            for ts in (True, False)]
+    assert envs[0].act is not None and envs[1].act is None
+    rng = np.random.default_rng(3)
+    for phase in range(2):
+        for env in envs:
+            env.reset()
+            if phase == 1:
+                case = make_case(E, N, N, 30, fire_p=0.02, hidden=False)
+                env.set_state(grid=case["grid"], fire_age=case["age"], wind_index=case["widx"])
+        for t in range(30):
+            act = np.stack([rng.integers(0, 9, E), rng.integers(0, 2, E)], axis=1)
+            outs = [env.step(act) for env in envs]
+            for k in (0,):
+                assert np.array_equal(outs[0][0][k].cpu().numpy(), outs[1][0][k].cpu().numpy()), f"{phase} {t}"
+            assert np.array_equal(envs[0].age[envs[0].cur].cpu().numpy(), envs[1].age[envs[1].cur].cpu().numpy())
+            assert np.array_equal(outs[0][1].cpu().numpy(), outs[1][1].cpu().numpy())
+            assert np.array_equal(outs[0][2].cpu().numpy(), outs[1][2].cpu().numpy())
+            if t == 20:
+                for env in envs:
+                    env.done[0] = 1
+                    env.conditional_reset()
+        # the map is exact: a tile is marked iff it holds a FIRE
+        g = envs[0].grid[envs[0].cur].cpu().numpy()
+        fire_tiles = (g == 2).reshape(E, N // 16, 16, N // 256, 256).any(axis=(2, 4)).reshape(E, -1)
+        assert np.array_equal(envs[0].act[envs[0].cur].cpu().numpy().astype(bool), fire_tiles)

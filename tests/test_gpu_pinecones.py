@@ -43,7 +43,7 @@ def test_pinecones_bit_exact_vs_oracle(device, E, H, W, seed):
     rsd = _t(rs.view(np.int32), torch.int32, device)
     counts = _t(c1, torch.int32, device)
     call("gca_alex_pinecones", pp, E, H, W, dev.ptr(gi), dev.ptr(go), dev.ptr(ao), dev.ptr(veg), dev.ptr(den),
-         dev.ptr(wi), dev.ptr(tb), dev.ptr(rsd), dev.ptr(counts), dev.stream_ptr())
+         dev.ptr(wi), dev.ptr(tb), dev.ptr(rsd), dev.ptr(counts), None, dev.stream_ptr())
     assert np.array_equal(go.cpu().numpy(), want_g)
     assert np.array_equal(ao.cpu().numpy(), want_a)
     assert np.array_equal(counts.cpu().numpy(), want_c)
