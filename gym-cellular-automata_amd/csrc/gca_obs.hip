@@ -24,6 +24,12 @@
 //   vis(v) = (v == 3 && !is_night) ? 0 : v   (the reference's literal 3, extension_utils.py:93).
 #include "gca_common.h"
 
+#ifndef GCA_OBS_DB
+#define GCA_OBS_DB 0  // 1: two RGB transposition buffers, one barrier per render round (A/B hook)
+#endif
+#ifndef GCA_OBS_RB
+#define GCA_OBS_RB 16  // rows per workgroup at W = 256 (A/B hook)
+#endif
 #ifndef GCA_OBS_NT
 #define GCA_OBS_NT 1  // non-temporal RGB stores (r01i A/B: 1.07 vs 1.10 ms per 4096 x 256^2)
 #endif
@@ -209,9 +215,11 @@ __global__ __launch_bounds__(256) void adv_observation_kernel(gca_obs_params p, 
     if ((W & 3) == 0) {
         // 256 threads x 4 cells per round; the 12 floats of each thread go through LDS so that every store
         // instruction writes 1 KiB of contiguous RGB (the rows of a block are contiguous in HBM)
-        __shared__ float4 OUT4[256 * 3];
+        __shared__ float4 OUT4s[(GCA_OBS_DB ? 2 : 1) * 256 * 3];
         const int wq = W >> 2;
+        int buf = 0;
         for (int base_q = 0; base_q < rows * wq; base_q += 256) {
+            float4* OUT4 = OUT4s + buf * (256 * 3);
             const int idx = base_q + (int)threadIdx.x;
             if (idx < rows * wq) {
                 const int lr = idx / wq, c0 = (idx - lr * wq) * 4, r = r0 + lr;
@@ -274,7 +282,10 @@ __global__ __launch_bounds__(256) void adv_observation_kernel(gca_obs_params p, 
 #endif
                 }
             }
-            __syncthreads();
+            if (GCA_OBS_DB)
+                buf ^= 1;  // the next round writes the other buffer: the barrier above orders this round's reads
+            else
+                __syncthreads();
         }
     } else {
         for (int idx = threadIdx.x; idx < rows * W; idx += blockDim.x) {
@@ -311,7 +322,7 @@ extern "C" int gca_adv_observation(const gca_obs_params* p, int mode, int E, int
     GCA_CHECK_ARG(W <= 16384, "adv_observation: W <= 16384");
     GCA_CHECK_ARG(((uintptr_t)rgb & 15u) == 0 && ((uintptr_t)grid & 3u) == 0 && ((uintptr_t)dousing & 3u) == 0,
                   "adv_observation: rgb must be 16-B and grid/dousing 4-B aligned");
-    const int RB = max(1, min(16, 32768 / W - 1));  // rows per block; (2 RB + 2) * W bytes of LDS (grid + dousing)
+    const int RB = max(1, min(GCA_OBS_RB, 32768 / W - 1));  // rows per block; (2 RB + 2) * W bytes of LDS (grid + dousing)
     const int bpe = (H + RB - 1) / RB;
     hipLaunchKernelGGL(adv_observation_kernel, dim3((unsigned)((int64_t)E * bpe)), dim3(256), (size_t)(2 * RB + 2) * W,
                        (hipStream_t)stream, *p, mode, H, W, RB, bpe, grid, dousing, pos, is_night, time_step, action,

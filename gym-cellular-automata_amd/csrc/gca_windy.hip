@@ -20,6 +20,10 @@
 //    Reward/done counts of the new grid are fused (wave reduction + 3 atomics).
 #include "gca_common.h"
 
+#ifndef GCA_WINDY_AHEAD
+#define GCA_WINDY_AHEAD 1  // windy_fast_kernel: row chunks in flight ahead of the one being computed (2, 4, 8: slower, r01o A/B)
+#endif
+
 // ------------------------------------------------------------------ dir mask
 __global__ void windy_dirmask_kernel(const double* __restrict__ wind, int64_t wind_stride,
                                      const double* __restrict__ roll, uint32_t k0, uint32_t k1,
@@ -150,25 +154,31 @@ __global__ __launch_bounds__(256) void windy_fast_kernel(uint8_t* __restrict__ b
         return make_uint4(0u, 0u, 0u, 0u);
     };
 
-    // prologue: chunk -1 (only the row just above the strip), chunk 0, chunk 1 in flight
+    // chunk c of the strip = rows s0 + c*RPW + g; chunk nT only for its first row (the strip's lower halo)
+    auto chunk_row = [&](int c) { return s0 + c * RPW + g; };
+    auto wanted = [&](int c) { return c < nT || (c == nT && g == 0); };
+    // prologue: chunk -1 (only the row just above the strip), chunk 0, and chunks 1..AHEAD in flight
     const int Rprev = s0 - RPW + g;
     Row16 prv = classify(load_row(Rprev, g == RPW - 1), Tp, Fp, g == RPW - 1 && Rprev >= 0);
-    int Rc = s0 + g;
-    Row16 cur = classify(load_row(Rc, true), Tp, Fp, Rc < H);
-    int Rn = s0 + RPW + g;
-    uint4 raw_next = load_row(Rn, nT > 1 || g == 0);
+    Row16 cur = classify(load_row(chunk_row(0), true), Tp, Fp, chunk_row(0) < H);
+    uint4 ring[GCA_WINDY_AHEAD];  // ring[u] holds chunk t + 1 when t % AHEAD == u
+#pragma unroll
+    for (int u = 0; u < GCA_WINDY_AHEAD; ++u) ring[u] = load_row(chunk_row(u + 1), wanted(u + 1));
 
     const int lane_up = (lane - LPR) & 63, lane_dn = (lane + LPR) & 63;
     const int lane_l = (lane - 1) & 63, lane_r = (lane + 1) & 63;
     const bool has_l = q > 0, has_r = q < LPR - 1;
 
     int32_t cntT = 0, cntF = 0, cntV = 0;
-    for (int t = 0; t < nT; ++t) {
-        const bool next_wanted = (t + 1 < nT) || g == 0;
-        Row16 nxt = classify(raw_next, Tp, Fp, next_wanted && Rn < H);
-        // issue the load two chunks ahead before computing this chunk
-        const int Rn2 = Rn + RPW;
-        raw_next = load_row(Rn2, (t + 2 < nT) || (t + 2 == nT && g == 0));
+    for (int t0 = 0; t0 < nT; t0 += GCA_WINDY_AHEAD) {
+#pragma unroll
+    for (int u = 0; u < GCA_WINDY_AHEAD; ++u) {
+        const int t = t0 + u;
+        if (t >= nT) break;  // wave-uniform
+        const int Rc = chunk_row(t), Rn = chunk_row(t + 1);
+        Row16 nxt = classify(ring[u], Tp, Fp, wanted(t + 1) && Rn < H);
+        // refill the slot just consumed: the load AHEAD + 1 chunks ahead, issued before computing this chunk
+        ring[u] = load_row(chunk_row(t + 1 + GCA_WINDY_AHEAD), wanted(t + 1 + GCA_WINDY_AHEAD));
 
         uint32_t up[4], dn[4];
 #pragma unroll
@@ -216,8 +226,7 @@ __global__ __launch_bounds__(256) void windy_fast_kernel(uint8_t* __restrict__ b
         }
         prv = cur;
         cur = nxt;
-        Rc = Rn;
-        Rn = Rn2;
+    }
     }
     if (counts) {
 #pragma unroll
