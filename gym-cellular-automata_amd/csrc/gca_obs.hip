@@ -76,10 +76,14 @@ __device__ __forceinline__ int ext_value(const gca_obs_params& p, const ObsCfg& 
     return ((k.on >> i) & 1u) ? transform(raw, bl, k.night, p.ext_skip_visibility[i], p.ext_skip_blur[i]) : 0;
 }
 
-__device__ __forceinline__ void render(const gca_obs_params& p, float* __restrict__ out, int v, int dous, bool night,
-                                       bool at_pos) {
+__device__ __forceinline__ int colour_kind(const gca_obs_params& p, int v, bool at_pos) {
+    return at_pos ? 3 : (v == p.tree ? 1 : (v == p.fire ? 2 : 0));
+}
+// colour of kind k (empty / tree / fire / position) with the dousing tint
+__device__ __forceinline__ void render_kind(const gca_obs_params& p, float* __restrict__ out, int k, int dous,
+                                            bool night) {
     const float(*col)[3] = night ? p.color_night : p.color_day;
-    const int k = at_pos ? 3 : (v == p.tree ? 1 : (v == p.fire ? 2 : 0));
+    const bool at_pos = k == 3;
     float rgb[3] = {col[k][0], col[k][1], col[k][2]};
     if (!at_pos && dous > 0) {
         const float s = dous == 1 ? 0.75f : 0.0f;
@@ -90,6 +94,10 @@ __device__ __forceinline__ void render(const gca_obs_params& p, float* __restric
     out[0] = rgb[0];
     out[1] = rgb[1];
     out[2] = rgb[2];
+}
+__device__ __forceinline__ void render(const gca_obs_params& p, float* __restrict__ out, int v, int dous, bool night,
+                                       bool at_pos) {
+    render_kind(p, out, colour_kind(p, v, at_pos), dous, night);
 }
 
 // Grid: (env, block of RB rows); 256 threads. The display selection (a scan from row 0 that normally
@@ -167,6 +175,15 @@ __global__ __launch_bounds__(256) void adv_observation_kernel(gca_obs_params p, 
     //      rows in LDS, every load issued before any is used: the render rounds below then read LDS only
     //      and never wait on HBM between their stores
     const bool stage_all = (W & 3) == 0;  // the 4-cells-per-thread path reads both arrays from LDS
+    // the block's 12 colours (kind x dousing 0 / 1 / >= 2) in LDS: the render rounds then index LDS instead of
+    // the kernel arguments (a per-lane index into them is a vector memory load, whose wait would also drain
+    // the previous round's stores)
+    __shared__ float4 COLT[12];
+    if (stage_all && threadIdx.x < 12) {
+        float c3[3];
+        render_kind(p, c3, (int)threadIdx.x / 3, (int)threadIdx.x % 3, k.night);
+        COLT[threadIdx.x] = make_float4(c3[0], c3[1], c3[2], 0.0f);
+    }
     if (stage_all || k.need_blur) {
         const bool al16 = ((((uintptr_t)grid) | ((uintptr_t)dousing)) & 15u) == 0;
         if ((W & 15) == 0 && al16) {
@@ -253,7 +270,11 @@ __global__ __launch_bounds__(256) void adv_observation_kernel(gca_obs_params p, 
 #pragma unroll
                     for (int i = 0; i < GCA_OBS_MAX_EXT; ++i)
                         if (sel == i) v = extv[i];
-                    render(p, out + 3 * j, v, (dw >> (8 * j)) & 0xFF, k.night, r == pr && c0 + j == pc);
+                    const float4 cl = COLT[3 * colour_kind(p, v, r == pr && c0 + j == pc) +
+                                           (int)min((dw >> (8 * j)) & 0xFFu, 2u)];
+                    out[3 * j] = cl.x;
+                    out[3 * j + 1] = cl.y;
+                    out[3 * j + 2] = cl.z;
                     if (channels) {
                         uint8_t* ch = channels + (e * HW + cell0 + j) * nch;
                         ch[0] = (uint8_t)base;
