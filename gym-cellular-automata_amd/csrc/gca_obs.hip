@@ -28,7 +28,7 @@
 #define GCA_OBS_DB 0  // 1: two RGB transposition buffers, one barrier per render round (A/B hook)
 #endif
 #ifndef GCA_OBS_RB
-#define GCA_OBS_RB 16  // rows per workgroup at W = 256 (A/B hook)
+#define GCA_OBS_RB 32  // rows per workgroup (r01o A/B at W = 256: 8 / 16 / 32 / 48 / 64 rows -> 0.90 / 0.76 / 0.72 / 0.84 / 0.89 ms)
 #endif
 #ifndef GCA_OBS_NT
 #define GCA_OBS_NT 1  // non-temporal RGB stores (r01i A/B: 1.07 vs 1.10 ms per 4096 x 256^2)
@@ -343,7 +343,8 @@ extern "C" int gca_adv_observation(const gca_obs_params* p, int mode, int E, int
     GCA_CHECK_ARG(W <= 16384, "adv_observation: W <= 16384");
     GCA_CHECK_ARG(((uintptr_t)rgb & 15u) == 0 && ((uintptr_t)grid & 3u) == 0 && ((uintptr_t)dousing & 3u) == 0,
                   "adv_observation: rgb must be 16-B and grid/dousing 4-B aligned");
-    const int RB = max(1, min(GCA_OBS_RB, 32768 / W - 1));  // rows per block; (2 RB + 2) * W bytes of LDS (grid + dousing)
+    // rows per block; (2 RB + 2) * W bytes of dynamic LDS (grid + dousing), at most 48 KiB
+    const int RB = max(1, min(GCA_OBS_RB, 24576 / W - 1));
     const int bpe = (H + RB - 1) / RB;
     hipLaunchKernelGGL(adv_observation_kernel, dim3((unsigned)((int64_t)E * bpe)), dim3(256), (size_t)(2 * RB + 2) * W,
                        (hipStream_t)stream, *p, mode, H, W, RB, bpe, grid, dousing, pos, is_night, time_step, action,
