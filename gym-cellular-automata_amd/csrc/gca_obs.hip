@@ -4,7 +4,7 @@
 //            apply_extensions (bulldozer/utils/extension_utils.py:89-196), the reset observation
 //            (advanced_bulldozer.py:401-411).
 //
-// Grid: one workgroup (256 threads) per (env, block of up to 16 rows):
+// Grid: one workgroup (256 threads) per (env, block of up to GCA_OBS_RB = 32 rows):
 //   A. (step mode, only when an extension channel can be non-zero) the first row holding a positive
 //      extension value — the reference's `has_extension` is a vmap over the ROWS of the channel-last
 //      (H, W, 3 + n_ext) stack, and the row index found is then used as the channel index (clamped to
