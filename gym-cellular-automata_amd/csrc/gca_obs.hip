@@ -27,6 +27,9 @@
 #ifndef GCA_OBS_DB
 #define GCA_OBS_DB 0  // 1: two RGB transposition buffers, one barrier per render round (A/B hook)
 #endif
+#ifndef GCA_OBS_WAVE
+#define GCA_OBS_WAVE 1  // wave-local RGB transposition (each wave stores its own 3 KiB), no barriers per round; 0: block-wide (r01p A/B: 0.713 vs 0.722 ms)
+#endif
 #ifndef GCA_OBS_RB
 #define GCA_OBS_RB 32  // rows per workgroup (r01o A/B at W = 256: 8 / 16 / 32 / 48 / 64 rows -> 0.90 / 0.76 / 0.72 / 0.84 / 0.89 ms)
 #endif
@@ -287,12 +290,21 @@ __global__ __launch_bounds__(256) void adv_observation_kernel(gca_obs_params p, 
                 OUT4[3 * threadIdx.x + 1] = make_float4(out[4], out[5], out[6], out[7]);
                 OUT4[3 * threadIdx.x + 2] = make_float4(out[8], out[9], out[10], out[11]);
             }
+#if GCA_OBS_WAVE
+            // a wave's 64 threads own 256 consecutive cells = 3 KiB of contiguous RGB: the transposition stays
+            // inside the wave (LDS operations of one wave complete in order), so no workgroup barrier
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#else
             __syncthreads();
+#endif
             const int n4 = 3 * min(256, rows * wq - base_q);
             float4* dst = reinterpret_cast<float4*>(rgb + (e * HW + (int64_t)r0 * W + 4 * (int64_t)base_q) * 3);
 #pragma unroll
             for (int j = 0; j < 3; ++j) {
-                const int q4 = (int)threadIdx.x + 256 * j;
+                const int q4 = GCA_OBS_WAVE ? 192 * ((int)threadIdx.x >> 6) + ((int)threadIdx.x & 63) + 64 * j
+                                            : (int)threadIdx.x + 256 * j;
                 if (q4 < n4) {
 #if GCA_OBS_NT
                     typedef float f4v __attribute__((ext_vector_type(4)));
@@ -303,10 +315,15 @@ __global__ __launch_bounds__(256) void adv_observation_kernel(gca_obs_params p, 
 #endif
                 }
             }
-            if (GCA_OBS_DB)
+            if (GCA_OBS_WAVE) {  // this round's LDS reads before the next round's writes (same wave)
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            } else if (GCA_OBS_DB) {
                 buf ^= 1;  // the next round writes the other buffer: the barrier above orders this round's reads
-            else
+            } else {
                 __syncthreads();
+            }
         }
     } else {
         for (int idx = threadIdx.x; idx < rows * W; idx += blockDim.x) {
