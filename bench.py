@@ -54,7 +54,33 @@ def parse():
     ap.add_argument("--headline-only", action="store_true",
                     help="only the headline loop (no RGB / episode-start loops): every alex_step launch is the "
                          "dense mid-episode one, so rocprofv3 per-kernel averages match kernel_ms")
+    ap.add_argument("--reps", type=int, default=5, help="timed repetitions of K steps; the median is reported")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU rehearsal of the N-rank launch: gloo ranks, env sharding and the episode-stats "
+                         "all-gather of gymca_amd.distributed, no GPU touched")
     return ap.parse_args()
+
+
+def _free_port():
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args):
+    """`bench.py --gpus N` started as a plain process: run N ranks (one per GPU) as CHILD processes through
+    torch.distributed.run and return their exit code. Nothing here touches the GPU (no exec either)."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__),
+           *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # RCCL over dmabuf IPC on this pool
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
 
 
 def setup_dist(args):
@@ -63,6 +89,9 @@ def setup_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py --gpus {args.gpus} but WORLD_SIZE={world}: launch N ranks with "
+                         f"torch.distributed.run or plain `python bench.py --gpus N`")
     torch.cuda.set_device(local)
     pg = None
     if world > 1:
@@ -70,8 +99,49 @@ def setup_dist(args):
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+        assert dist.get_world_size() == args.gpus
         pg = dist
     return world, rank, torch.device("cuda", local), pg
+
+
+def dry_run(args):
+    """The distributed plumbing of the bench on CPU (gloo): each rank takes its env shard of the global batch
+    (gymca_amd.distributed.shard), fills its per-env episode stats from its GLOBAL env ids, all-gathers them
+    with the bench's own gather (distributed.all_gather_stats) and checks the gathered rank order."""
+    import torch
+    import torch.distributed as dist
+
+    from gymca_amd import distributed as gd
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--dry-run --gpus {args.gpus} but WORLD_SIZE={world}")
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    total = args.envs * world
+    off, cnt = gd.shard(total, world, rank)
+    gid = torch.arange(off, off + cnt)
+    done = (gid % 3 == 0).to(torch.uint8)
+    ret = -gid.to(torch.float32) / 8
+    length = gid.to(torch.int32) + 1
+    d, r, ln = gd.all_gather_stats(done, ret, length)
+    allid = torch.arange(total)
+    ok = (torch.equal(d, (allid % 3 == 0).to(torch.uint8)) and torch.equal(r, -allid.to(torch.float32) / 8)
+          and torch.equal(ln, allid.to(torch.int32) + 1))
+    oks = [None] * world
+    if world > 1:
+        dist.all_gather_object(oks, (rank, off, cnt, bool(ok)))
+    else:
+        oks = [(rank, off, cnt, bool(ok))]
+    if rank == 0:
+        print(json.dumps({"metric": "dry-run", "n_gpus": world, "backend": "gloo" if world > 1 else "none",
+                          "dry_run": True, "ranks": [{"rank": a, "env_offset": b, "envs": c, "gather_ok": o}
+                                                     for a, b, c, o in oks],
+                          "gather_ok": all(o for *_, o in oks)}))
+    if world > 1:
+        dist.destroy_process_group()
+    return 0 if all(o for *_, o in oks) else 1
 
 
 def synthetic_state(env, rank, device):
@@ -94,30 +164,45 @@ def synthetic_state(env, rank, device):
     env.set_state(grid=grid, fire_age=age, wind_index=widx)
 
 
-def timed_loop(step_fn, K, W, pg, device):
+def timed_loop(step_fn, K, W, pg, device, reps=1, detail=None, prepare=None):
+    """W untimed steps, then `reps` repetitions of EXACTLY K steps, each bracketed by barrier + synchronize on
+    both sides, max over ranks. Returns (median seconds per K steps, mean kernel seconds from the events
+    step_fn records). `prepare` (optional) restores the workload's starting state before the warm-up and
+    before every repetition (untimed), so each repetition times the same K steps of the workload rather than
+    an ever later stretch of one trajectory. `detail` (dict, optional) receives every repetition's ms per step."""
     import torch
 
+    if prepare is not None:
+        prepare()
     for _ in range(W):
         step_fn(None)
-    torch.cuda.synchronize(device)
-    if pg is not None:
-        pg.barrier()
-    torch.cuda.synchronize(device)
-    events = []
-    t0 = time.perf_counter()
-    for _ in range(K):
-        step_fn(events)
-    torch.cuda.synchronize(device)
-    if pg is not None:
-        pg.barrier()
-    torch.cuda.synchronize(device)
-    dt = time.perf_counter() - t0
+    events, dts = [], []
+    for _ in range(max(1, reps)):
+        if prepare is not None:
+            prepare()
+        torch.cuda.synchronize(device)
+        if pg is not None:
+            pg.barrier()
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        for _ in range(K):
+            step_fn(events)
+        torch.cuda.synchronize(device)
+        if pg is not None:
+            pg.barrier()
+        torch.cuda.synchronize(device)
+        dt = time.perf_counter() - t0
+        if pg is not None:
+            t = torch.tensor([dt], dtype=torch.float64, device=device)
+            pg.all_reduce(t, op=pg.ReduceOp.MAX)
+            dt = float(t.item())
+        dts.append(dt)
     kern = [a.elapsed_time(b) * 1e-3 for a, b in events]
-    if pg is not None:
-        t = torch.tensor([dt], dtype=torch.float64, device=device)
-        pg.all_reduce(t, op=pg.ReduceOp.MAX)
-        dt = float(t.item())
-    return dt, (sum(kern) / len(kern) if kern else None)
+    med = sorted(dts)[len(dts) // 2]
+    if detail is not None:
+        detail["reps_ms_per_step"] = [d / K * 1e3 for d in dts]
+        detail["median_of"] = len(dts)
+    return med, (sum(kern) / len(kern) if kern else None)
 
 
 def bench_alex(args, world, rank, device, pg):
@@ -134,8 +219,8 @@ def bench_alex(args, world, rank, device, pg):
     env.reset()
     synthetic_state(env, rank, device)
     action = torch.zeros((E, 2), dtype=torch.int32, device=device)
-    gathered = [torch.empty(E * 5, dtype=torch.uint8, device=device) for _ in range(world)] if world > 1 else None
     st = dev.stream_ptr(device)
+    from gymca_amd import distributed as gd
 
     def step(events):
         call("gca_random_actions", dev.ptr(action), E, env.env_offset, 7, dev.ptr(env.rng_step), st)
@@ -147,13 +232,14 @@ def bench_alex(args, world, rank, device, pg):
             events.append((a, b))
         else:
             env.ca_step()
-        env.post_step(action)
-        if gathered is not None and args.gather == "step":
-            # RCCL all-gather of the per-env done mask + reward
-            payload = torch.cat([env.done, env.reward.view(torch.uint8)])
-            pg.all_gather(gathered, payload)
+        env.post_step(action, stats=True)  # + info steps_elapsed / reward_accumulated, fused
+        if world > 1 and args.gather == "step":
+            # RCCL all-gather of the per-env episode stats (done u8 | return f32 | length i32)
+            gd.all_gather_stats(env.done, env.reward_accumulated, env.steps_elapsed)
 
-    dt, kern = timed_loop(step, args.steps, args.warmup, pg, device)
+    detail = {}
+    prep = lambda: synthetic_state(env, rank, device)  # every repetition times K steps from the C3 state
+    dt, kern = timed_loop(step, args.steps, args.warmup, pg, device, reps=args.reps, detail=detail, prepare=prep)
     cells = world * E * N * N * args.steps
     res = {
         "value": cells / dt,
@@ -163,6 +249,7 @@ def bench_alex(args, world, rank, device, pg):
         "achieved_gbs": ALEX_BYTES[args.slope_layout] * E * N * N / kern / 1e9,
         "survey_equiv_gbs": ALEX_BYTES_PER_CELL * E * N * N / kern / 1e9,
         "fires_left": int((env.counts[:, 2] > 0).sum().item()),
+        "timing": detail,
     }
     if args.headline_only:
         return res
@@ -182,7 +269,7 @@ def bench_alex(args, world, rank, device, pg):
         else:
             env.render_observation(action3)
 
-    dt_rgb, kern_rgb = timed_loop(step_rgb, args.steps, args.warmup, pg, device)
+    dt_rgb, kern_rgb = timed_loop(step_rgb, args.steps, args.warmup, pg, device, reps=3, prepare=prep)
     res["with_rgb_observation"] = {"env_steps_per_s": world * E * args.steps / dt_rgb,
                                    "cell_updates_per_s": world * E * N * N * args.steps / dt_rgb,
                                    "obs_kernel_ms": kern_rgb * 1e3,
@@ -191,14 +278,12 @@ def bench_alex(args, world, rank, device, pg):
     # the same env from its reset state (two burning cells per env, advanced_bulldozer.py:650-688): a
     # real episode's first steps, where the fire-sparsity skip leaves most waves the 7 B/cell of
     # grid/age/dousing traffic. Reported separately; the headline above is the dense mid-episode state.
-    env.reset()
-    dt_sp, kern_sp = timed_loop(step, args.steps, args.warmup, pg, device)
+    dt_sp, kern_sp = timed_loop(step, args.steps, args.warmup, pg, device, reps=3, prepare=env.reset)
     res["episode_start"] = {"cell_updates_per_s": world * E * N * N * args.steps / dt_sp,
                             "kernel_ms": kern_sp * 1e3, "state": "reset state (2 fires per env), fire-sparsity skip"}
     # the same episode start with the opt-in tile activity map (tiles without fire nearby copied, not stepped)
     env.set_tile_skip(True)
-    env.reset()
-    dt_ts, kern_ts = timed_loop(step, args.steps, args.warmup, pg, device)
+    dt_ts, kern_ts = timed_loop(step, args.steps, args.warmup, pg, device, reps=3, prepare=env.reset)
     res["episode_start"]["tile_skip"] = {"cell_updates_per_s": world * E * N * N * args.steps / dt_ts,
                                          "kernel_ms": kern_ts * 1e3}
     env.set_tile_skip(args.tile_skip)
@@ -207,9 +292,10 @@ def bench_alex(args, world, rank, device, pg):
 
 def bench_config4(args, world, rank, device, pg):
     """BASELINE config 4: AdvancedBulldozer 256x256 with the hidden foliage / altitude layers
-    (use_hidden=True), 4096 envs per GPU. The layers come from the init_utils restatement on a
-    seeded legacy stream (same draws as the reference after np.random.seed), altitude arithmetic and
-    get_slope on the device; then the same timed step as the headline with a mid-episode state."""
+    (use_hidden=True), 4096 envs per GPU. The layers follow init_utils.py:10-116's recipe drawn on the device
+    (hidden_rng="philox", gca_hidden_init; the np.random-stream restatement is the env's default and takes
+    seconds at this size), altitude arithmetic and get_slope on the device; then the same timed step as the
+    headline from the same mid-episode state."""
     import numpy as np
     import torch
 
@@ -220,7 +306,7 @@ def bench_config4(args, world, rank, device, pg):
     E, N = args.envs, args.size
     t0 = time.perf_counter()
     env = AdvancedForestFireBulldozerEnv(N, N, key=2, num_envs=E, use_hidden=True, device=device,
-                                         env_offset=rank * E, hidden_rng=np.random.RandomState(2 + rank),
+                                         env_offset=rank * E, hidden_rng="philox", observation="grid",
                                          slope_layout=args.slope_layout)
     torch.cuda.synchronize(device)
     init_s = time.perf_counter() - t0
@@ -241,15 +327,16 @@ def bench_config4(args, world, rank, device, pg):
             env.ca_step()
         env.post_step(action)
 
-    dt, kern = timed_loop(step, args.steps, args.warmup, pg, device)
+    dt, kern = timed_loop(step, args.steps, args.warmup, pg, device, reps=3,
+                          prepare=lambda: synthetic_state(env, rank, device))
     out = {"config": "AdvancedBulldozer 256x256, hidden foliage/altitude layers (use_hidden=True), 4096 envs/GPU",
            "cell_updates_per_s": world * E * N * N * args.steps / dt,
            "env_steps_per_s": world * E * args.steps / dt,
            "kernel_ms": kern * 1e3,
            "achieved_gbs": ALEX_BYTES[args.slope_layout] * E * N * N / kern / 1e9,
            "init_s": init_s,
-           "init": "patches + altitude draws on the host (legacy np.random order), altitude arithmetic + "
-                   "get_slope + exp on the device"}
+           "init": "hidden_rng='philox': patches, zero fill, noise, hills and slopes drawn on the device "
+                   "(gca_hidden_init, keyed by global env id), altitude arithmetic + get_slope + exp on the device"}
     del env
     torch.cuda.empty_cache()
     return out
@@ -343,12 +430,13 @@ def bench_windy512(args, world, rank, device, pg):
     from gymca_amd.forest_fire.bulldozer import BatchedForestFireBulldozerEnv
     from gymca_amd.graph import StepGraph
 
+    from gymca_amd import distributed as gd
+
     E, N = 1024, 512
     env = BatchedForestFireBulldozerEnv(E, N, N, device=device, seed=0x5EED5, env_offset=rank * E,
                                         materialize_obs=False)
     env.reset()
     action = torch.zeros((E, 2), dtype=torch.int32, device=device)
-    gathered = [torch.empty(E * 9, dtype=torch.uint8, device=device) for _ in range(world)] if world > 1 else None
 
     def one_step():
         call("gca_random_actions", dev.ptr(action), E, env.env_offset, 11, dev.ptr(env.rng_step),
@@ -356,8 +444,8 @@ def bench_windy512(args, world, rank, device, pg):
         env.step(action)
 
     def gather():
-        if gathered is not None:
-            pg.all_gather(gathered, torch.cat([env.done, env.reward.view(torch.uint8)]))
+        if world > 1:  # RCCL all-gather of done u8 | reward f32 | length i32 per env (gymca_amd.distributed)
+            gd.all_gather_stats(env.done, env.reward, env.steps_elapsed)
 
     K = max(args.steps, 40)
 
@@ -375,10 +463,54 @@ def bench_windy512(args, world, rank, device, pg):
 
     Kg = max(K // G, 5)
     dt_g, _ = timed_loop(seg, Kg, 2, pg, device)
+    # CA-only at HBM scale: one forced Windy step of every env, 268 MB per buffer (beyond the 256 MB
+    # Infinity Cache, unlike config 2's 64 MiB pair), dense {0:.1, 3:.6, 25:.3}, beside a same-size copy
+    ca = windy_ca_only(env, K, args.warmup, pg, device)
     return {"config": "ForestFireBulldozer 512x512, 1024 envs/GPU (BASELINE config 5 at 8 GPUs), WindyForestFire",
             "env_steps_per_s": world * E * Kg * G / dt_g,
             "env_steps_per_s_eager_gather_every_step": world * E * K / dt_eager,
-            "gather": "RCCL all_gather of done u8 + reward f64 per env" if world > 1 else "none (1 GPU)"}
+            "gather": ("RCCL all_gather of done u8 | reward f32 | length i32 per env (gymca_amd.distributed), "
+                       f"world {world}") if world > 1 else "none (1 GPU)",
+            "ca_only_cell_updates_per_s": world * E * N * N / ca["kernel_s"],
+            "ca_kernel_ms": ca["kernel_s"] * 1e3,
+            "ca_achieved_gbs": WINDY_BYTES_PER_CELL * E * N * N / ca["kernel_s"] / 1e9,
+            "ca_roofline_frac": WINDY_BYTES_PER_CELL * E * N * N / ca["kernel_s"] / 1e9 / HBM_PEAK_GBS,
+            "same_size_copy_ms": ca["copy_s"] * 1e3,
+            "ca_frac_of_same_size_copy": ca["copy_s"] / ca["kernel_s"]}
+
+
+def windy_ca_only(env, K, W, pg, device):
+    """Mean duration of one forced Windy CA step over every env of `env` (dense state, random direction masks)
+    and of a device copy of the same bytes, both from HIP events."""
+    import torch
+
+    E, H, N = env.num_envs, env.nrows, env.ncols
+    g = env.grids()
+    u = torch.rand(g.shape, device=device)
+    g = torch.where(u < 0.1, 0, torch.where(u < 0.7, 3, 25)).to(torch.uint8)
+    env.buf[0].copy_(g)
+    del g, u
+    env.parity.zero_()
+    env.dir_mask.copy_(torch.randint(0, 256, (E,), dtype=torch.uint8, device=device))
+
+    def timed(fn):
+        def f(events):
+            if events is not None:
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+                fn()
+                b.record()
+                events.append((a, b))
+            else:
+                fn()
+        return f
+
+    _, kern = timed_loop(timed(env.ca_step_all), K, W, pg, device)
+    src = torch.empty(E * H * N, dtype=torch.uint8, device=device)
+    dst = torch.empty_like(src)
+    _, kern_copy = timed_loop(timed(lambda: dst.copy_(src)), K, W, pg, device)
+    del src, dst
+    return {"kernel_s": kern, "copy_s": kern_copy}
 
 
 def _cpu_model():
@@ -477,6 +609,146 @@ def windy_cpu_baseline(seconds=3.0):
             "sample": f"1 env 256x256, {steps} steps of the scipy restatement + cell count"}
 
 
+def _windy_worker(args_tuple):
+    """One process of the all-core Windy CPU leg: the scipy restatement + cell count on one 256x256 env."""
+    seconds, seed = args_tuple
+    import numpy as np
+
+    from gymca_amd.forest_fire.bulldozer.bulldozer import DEFAULT_WIND, parse_wind
+    from oracle import windy as owindy
+
+    rng = np.random.default_rng(seed)
+    grid = rng.choice(np.array([0, 3, 25]), size=(256, 256), p=[0.1, 0.6, 0.3])
+    wind = parse_wind(DEFAULT_WIND)
+    steps, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        grid = owindy.windy_step(grid, wind, rng.random((3, 3)))
+        np.unique(grid, return_counts=True)
+        steps += 1
+    return steps, time.perf_counter() - t0
+
+
+def windy_cpu_all_cores(seconds=3.0):
+    """BASELINE.md CPU plan (ii): the Windy restatement on every core this job may use, one process per core,
+    envs split evenly. Forked BEFORE this process touches the GPU (main() runs the CPU legs first)."""
+    import multiprocessing as mp
+
+    n = _cpu_threads()
+    with mp.get_context("fork").Pool(n) as pool:
+        res = pool.map(_windy_worker, [(seconds, 100 + i) for i in range(n)])
+    rate = sum(256 * 256 * st / dt for st, dt in res)
+    return {"value": rate, "unit": "cell-updates/s", "cores": n, "kind": "port",
+            "sample": f"{n} processes x 1 env 256x256, {sum(st for st, _ in res)} steps of the scipy restatement "
+                      f"+ cell count in {seconds:.0f} s"}
+
+
+def bulldozer_cpu_baseline(seconds=3.0, N=256):
+    """The ForestFireBulldozer 256x256 env loop on one core, the reference's CPU path restated (oracle.windy:
+    scipy convolve2d CA passes, RepeatCA time, Move/Modify) with the reference's Counter-based cell count per
+    step (ca_env.py:94-99) and random actions; reset when the fire is out."""
+    from collections import Counter
+
+    import numpy as np
+
+    from gymca_amd.forest_fire.bulldozer.bulldozer import DEFAULT_WIND, bulldozer_timings, parse_wind
+    from oracle import windy as owindy
+
+    rng = np.random.default_rng(11)
+    t_move, t_shoot = bulldozer_timings(N, N)
+
+    def fresh():
+        g = rng.choice(np.array([0, 3]), size=(N, N), p=[0.1, 0.9])
+        g[3 * N // 4, N // 4] = 25
+        return owindy.BulldozerOracle([g], [(N // 4, 3 * N // 4)], parse_wind(DEFAULT_WIND), t_move, t_shoot, 0.001,
+                                      seed=rng.integers(1 << 62))
+
+    env, steps, resets = fresh(), 0, 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        env.step([(int(rng.integers(0, 9)), int(rng.integers(0, 2)))])
+        c = Counter(env.grids[0].ravel().tolist())  # the reference's count_cells
+        steps += 1
+        if not c[25]:
+            env, resets = fresh(), resets + 1
+    dt = time.perf_counter() - t0
+    return {"value": steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"1 env {N}x{N}, {steps} env steps (random actions, {resets} resets) of the numpy/scipy "
+                      f"restatement + Counter cell count"}
+
+
+def helicopter_cpu_baseline(steps=1000):
+    """BASELINE config 1 on one core: ForestFireHelicopter 5x5, seed 0, 1000 steps, actions k % 9 — the
+    Drossel-Schwabl per-cell loop restated (oracle.drossel, the reference's draw order), CA every
+    max_freeze + 1 steps, Move/Modify {FIRE: EMPTY} (helicopter.py:220-236), reward from cell counts."""
+    import numpy as np
+
+    from oracle import drossel
+    from oracle import windy as owindy
+
+    rng = np.random.default_rng(0)
+    grid = rng.choice(np.array([0, 1, 2]), size=(5, 5))
+    pos, freeze, max_freeze = (2, 2), 2, 2
+    t0 = time.perf_counter()
+    for k in range(steps):
+        if freeze == 0:
+            grid = drossel.ds_step(grid, 0.033, 0.333, rng)
+            freeze = max_freeze
+        else:
+            freeze -= 1
+        pos = owindy.move(pos, k % 9, 5, 5)
+        if grid[pos] == 2:
+            grid[pos] = 0
+        counts = np.bincount(grid.ravel(), minlength=3) / 25.0
+        float(np.dot([0.0, 1.0, -1.0], counts))
+    dt = time.perf_counter() - t0
+    return {"value": steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"1 env 5x5, {steps} steps, actions k % 9 (Drossel-Schwabl restatement, oracle/drossel.py)"}
+
+
+def bench_dropins(device):
+    """What a reference user swaps in, one env each (no batching): the ForestFireBulldozerEnv drop-in at 256x256
+    with random actions (reference: 366 env-steps/s on one core) and BASELINE config 1,
+    ForestFireHelicopterEnv(5, 5) for 1000 steps with actions k % 9 (helicopter.py:220-236)."""
+    import numpy as np
+    import torch
+
+    from gymca_amd.forest_fire.bulldozer import ForestFireBulldozerEnv
+    from gymca_amd.forest_fire.helicopter import ForestFireHelicopterEnv
+
+    out = {}
+    env = ForestFireBulldozerEnv(256, 256)
+    env.reset(seed=0)
+    rng = np.random.default_rng(3)
+    for _ in range(20):
+        env.step((int(rng.integers(0, 9)), int(rng.integers(0, 2))))
+    torch.cuda.synchronize(device)
+    steps, resets, ca = 0, 0, 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < 3.0:
+        _, _, term, _, _ = env.step((int(rng.integers(0, 9)), int(rng.integers(0, 2))))
+        steps += 1
+        if term:
+            env.reset()
+            resets += 1
+    torch.cuda.synchronize(device)
+    dt = time.perf_counter() - t0
+    out["bulldozer_256"] = {"env_steps_per_s": steps / dt, "steps": steps, "resets": resets,
+                            "note": "ForestFireBulldozerEnv(256, 256) drop-in, numpy int64 obs per step, grid "
+                                    "device-resident, one cell count per step"}
+    heli = ForestFireHelicopterEnv(5, 5)
+    heli.reset(seed=0)
+    heli.step(0)
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for k in range(1000):
+        heli.step(k % 9)
+    torch.cuda.synchronize(device)
+    dt = time.perf_counter() - t0
+    out["helicopter_5x5"] = {"env_steps_per_s": 1000 / dt, "steps": 1000,
+                             "note": "BASELINE config 1: ForestFireHelicopterEnv(5, 5) drop-in, actions k % 9"}
+    return out
+
+
 def measured_traffic(args):
     """HBM bytes per alex_step launch from the committed rocprofv3 PMC summary
     (profiles/pmc_traffic.json, written by scripts/pmc_summary.py: 2*FETCH_SIZE + WRITE_SIZE,
@@ -518,6 +790,21 @@ def copy_bandwidth(device, nbytes=2 << 30, reps=10):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(args)  # N child ranks; this process never touches the GPU
+    if args.dry_run:
+        return dry_run(args)
+    world_env, rank_env = int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0"))
+    if world_env != args.gpus:
+        raise SystemExit(f"bench.py --gpus {args.gpus} but WORLD_SIZE={world_env}: launch it as plain "
+                         f"`python bench.py --gpus N` (it starts the N ranks) or through torch.distributed.run")
+    cpu = cpu_legs = None
+    if rank_env == 0 and world_env == 1 and not args.no_cpu_baseline:
+        # CPU legs first: the all-core Windy leg forks worker processes, which must happen before this
+        # process initialises the GPU
+        cpu = cpu_baseline(args)
+        cpu_legs = {"windy_1core": windy_cpu_baseline(), "windy_all_cores": windy_cpu_all_cores(),
+                    "bulldozer_env_256": bulldozer_cpu_baseline(), "helicopter_5x5": helicopter_cpu_baseline()}
     world, rank, device, pg = setup_dist(args)
     import torch
 
@@ -529,11 +816,14 @@ def main():
     config4 = None if args.no_secondary else bench_config4(args, world, rank, device, pg)
     secondary = None if args.no_secondary else bench_windy(args, world, rank, device, pg)
     config5 = None if args.no_secondary else bench_windy512(args, world, rank, device, pg)
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args)
+    dropins = None if (args.no_secondary or world > 1) else bench_dropins(device)
+    if cpu_legs is not None:
         if secondary is not None:
-            secondary["cpu_baseline"] = windy_cpu_baseline()
+            secondary["cpu_baseline"] = cpu_legs["windy_1core"]
+            secondary["cpu_baseline_all_cores"] = cpu_legs["windy_all_cores"]
+        if dropins is not None:
+            dropins["bulldozer_256"]["cpu_baseline"] = cpu_legs["bulldozer_env_256"]
+            dropins["helicopter_5x5"]["cpu_baseline"] = cpu_legs["helicopter_5x5"]
     traffic = measured_traffic(args)
     copy_gbs = copy_bandwidth(device)
     if rank == 0:
@@ -553,14 +843,18 @@ def main():
             "config": {"workload": "AdvancedForestFireBulldozer 256x256, 4096 envs/GPU, Alexandridis rule, "
                                    "use_hidden=False (BASELINE config 3)",
                        "envs_per_gpu": args.envs, "grid": [args.size, args.size],
-                       "parallelism": f"env-sharded x{world}" + (", RCCL all_gather done/reward per step"
+                       "parallelism": f"env-sharded x{world}" + (", RCCL all_gather of done/return/length per step"
                                                                   if world > 1 and args.gather == "step" else "")},
+            "rccl_world": world if pg is not None else None,
+            "envs_total": world * args.envs,
+            "timing": dict(alex["timing"], note="value / ms_per_step = the median of the repetitions, each "
+                                                "exactly `steps` steps between barrier + synchronize"),
             "env_steps_per_s": alex["env_steps_per_s"],
             "episode_start": alex.get("episode_start"),
             "with_rgb_observation": alex.get("with_rgb_observation"),
             # achieved = SURVEY.md §8d's algorithmic figure (41 B per cell-update, "independent of the build's
             # actual layout") x cells / the kernel's mean launch time; the bytes this build actually moves
-            # (edge-slope layout: 25 B/cell) and the PMC traffic are reported beside it
+            # (packed layout: 23.125 B/cell) and the PMC traffic are reported beside it
             "roofline": {"bound": "hbm", "achieved": alex["survey_equiv_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": alex["survey_equiv_gbs"] / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "alex_step_kernel" + {"packed": "<ES, PK>", "edge": "<ES>", "planes": ""}[args.slope_layout],
@@ -571,17 +865,21 @@ def main():
                          "moved_gbs": alex["achieved_gbs"],
                          "moved_frac": alex["achieved_gbs"] / HBM_PEAK_GBS,
                          "traffic_bytes_per_cell": traffic / (args.envs * args.size * args.size) if traffic else None,
+                         "traffic_gbs": traffic / (alex["kernel_ms"] * 1e-3) / 1e9 if traffic else None,
+                         "traffic_frac": traffic / (alex["kernel_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS if traffic else None,
                          "device_copy_gbs": copy_gbs,
                          "moved_frac_of_device_copy": alex["achieved_gbs"] / copy_gbs},
             "cpu_baseline": cpu,
             "secondary": secondary,
             "config4": config4,
             "config5": config5,
+            "dropins": dropins,
         }
         print(json.dumps(out))
     if pg is not None:
         pg.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

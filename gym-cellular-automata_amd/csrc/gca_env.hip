@@ -158,7 +158,8 @@ __global__ void advenv_post_kernel(gca_advenv_params p, const int32_t* __restric
                                    uint8_t* __restrict__ dousing, uint16_t* __restrict__ dous_bits, int H, int W,
                                    const int32_t* __restrict__ counts,
                                    uint32_t* __restrict__ rng_step, float* __restrict__ reward,
-                                   uint8_t* __restrict__ done, int E) {
+                                   uint8_t* __restrict__ done, float* __restrict__ steps_elapsed,
+                                   float* __restrict__ reward_acc, int E) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= E) return;
     const uint32_t step = rng_step[e];
@@ -188,22 +189,27 @@ __global__ void advenv_post_kernel(gca_advenv_params p, const int32_t* __restric
     // _award (:597-630): -(f / (t + f + 1e-8)) in f32; _is_done (:632-633)
     const int t = counts[3 * e + 1], f = counts[3 * e + 2];
     const float denom = __fadd_rn((float)(t + f), 1e-8f);
-    reward[e] = -__fdiv_rn((float)f, denom);
+    const float rw = -__fdiv_rn((float)f, denom);
+    reward[e] = rw;
     done[e] = f == 0 ? 1 : 0;
+    if (steps_elapsed) steps_elapsed[e] = __fadd_rn(steps_elapsed[e], 1.0f);
+    if (reward_acc) reward_acc[e] = __fadd_rn(reward_acc[e], rw);
     rng_step[e] = step + 1u;
 }
 
 extern "C" int gca_advenv_post(const gca_advenv_params* p, const int32_t* action, int32_t* pos, float* accu,
                                int32_t* wind_index, int32_t* time_step, int32_t* is_night, uint8_t* dousing,
                                uint16_t* dous_bits, int H, int W, const int32_t* counts, uint32_t* rng_step,
-                               float* reward, uint8_t* done, int E, void* stream) {
+                               float* reward, uint8_t* done, float* steps_elapsed, float* reward_accumulated, int E,
+                               void* stream) {
     GCA_CHECK_ARG(p && action && pos && accu && wind_index && time_step && is_night && dousing && counts && rng_step &&
                       reward && done && E > 0,
                   "advenv_post: null argument");
     GCA_CHECK_ARG(p->n_winds > 0, "advenv_post: n_winds > 0");
     GCA_CHECK_ARG(!dous_bits || (W % 16 == 0), "advenv_post: dousing bits need W % 16 == 0");
     hipLaunchKernelGGL(advenv_post_kernel, ENV_GRID(E), 0, (hipStream_t)stream, *p, action, pos, accu, wind_index,
-                       time_step, is_night, dousing, dous_bits, H, W, counts, rng_step, reward, done, E);
+                       time_step, is_night, dousing, dous_bits, H, W, counts, rng_step, reward, done, steps_elapsed,
+                       reward_accumulated, E);
     GCA_CHECK_LAUNCH("advenv_post");
     return GCA_OK;
 }

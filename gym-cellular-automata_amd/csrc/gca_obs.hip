@@ -114,10 +114,12 @@ __global__ __launch_bounds__(256) void adv_observation_kernel(gca_obs_params p, 
                                                               const int32_t* __restrict__ is_night,
                                                               const int32_t* __restrict__ time_step,
                                                               const int32_t* __restrict__ action, int action_stride,
-                                                              float* __restrict__ rgb, uint8_t* __restrict__ channels) {
+                                                              float* __restrict__ rgb, uint8_t* __restrict__ channels,
+                                                              const uint8_t* __restrict__ env_mask) {
     extern __shared__ uint8_t T[];  // [(RB + 2) * W] grid rows r0-1 .. r0+RB (edge-clamped), then [RB * W] dousing
     uint8_t* D = T + (RB + 2) * W;
     const int e = blockIdx.x / blocks_per_env;
+    if (env_mask && !env_mask[e]) return;  // whole block: envs outside the mask keep their observation
     const int r0 = (blockIdx.x - e * blocks_per_env) * RB;
     const int rows = min(RB, H - r0);
     const int64_t HW = (int64_t)H * W;
@@ -351,7 +353,7 @@ __global__ __launch_bounds__(256) void adv_observation_kernel(gca_obs_params p, 
 extern "C" int gca_adv_observation(const gca_obs_params* p, int mode, int E, int H, int W, const uint8_t* grid,
                                    const uint8_t* dousing, const int32_t* pos, const int32_t* is_night,
                                    const int32_t* time_step, const int32_t* action, int action_stride, float* rgb,
-                                   uint8_t* channels, void* stream) {
+                                   uint8_t* channels, const uint8_t* env_mask, void* stream) {
     GCA_CHECK_ARG(p && grid && pos && is_night && rgb && E > 0 && H > 0 && W > 0, "adv_observation: bad arguments");
     GCA_CHECK_ARG(mode == 0 || mode == 1, "adv_observation: mode is 0 (step) or 1 (reset)");
     GCA_CHECK_ARG(p->n_ext >= 0 && p->n_ext <= GCA_OBS_MAX_EXT, "adv_observation: 0..4 extension channels");
@@ -365,7 +367,7 @@ extern "C" int gca_adv_observation(const gca_obs_params* p, int mode, int E, int
     const int bpe = (H + RB - 1) / RB;
     hipLaunchKernelGGL(adv_observation_kernel, dim3((unsigned)((int64_t)E * bpe)), dim3(256), (size_t)(2 * RB + 2) * W,
                        (hipStream_t)stream, *p, mode, H, W, RB, bpe, grid, dousing, pos, is_night, time_step, action,
-                       action_stride, rgb, channels);
+                       action_stride, rgb, channels, env_mask);
     GCA_CHECK_LAUNCH("adv_observation");
     return GCA_OK;
 }

@@ -23,6 +23,8 @@ TAG_INIT = 0x494E4954
 TAG_DS_CELL = 0x44534345
 TAG_PINE = 0x50494E45
 TAG_PINE_AGE = 0x50494E41
+TAG_HIDDEN = 0x48494444
+TAG_HIDDEN_CELL = 0x48494443
 GCA_PINE_MAX = 8
 GCA_PINE_CDF = 17
 
@@ -167,13 +169,15 @@ _SIGNATURES = {
     "gca_alex_pack_layers": ([P, P, P, P, P, c_int, c_int, c_int, P], c_int),
     "gca_alex_edge_slope_coalesce": ([P, P, c_int, c_int, c_int, P], c_int),
     "gca_alex_edge_factors": ([P, P, P, c_int64, P], c_int),
-    "gca_adv_observation": ([POINTER(ObsParams), c_int, c_int, c_int, c_int, P, P, P, P, P, P, c_int, P, P, P],
+    "gca_adv_observation": ([POINTER(ObsParams), c_int, c_int, c_int, c_int, P, P, P, P, P, P, c_int, P, P, P, P],
                             c_int),
     "gca_alex_altitude_apply": ([P, c_int, c_int, c_int, P, P, P, P, P], c_int),
-    "gca_advenv_post": ([POINTER(AdvEnvParams), P, P, P, P, P, P, P, P, c_int, c_int, P, P, P, P, c_int, P], c_int),
+    "gca_advenv_post": ([POINTER(AdvEnvParams), P, P, P, P, P, P, P, P, c_int, c_int, P, P, P, P, P, P, c_int, P],
+                        c_int),
     "gca_reset_where": ([P, c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, P, P, P], c_int),
     "gca_fill_categorical": ([P, c_int64, c_int, c_int, c_uint64, P, P, c_int, P], c_int),
     "gca_random_actions": ([P, c_int, c_int, c_uint64, P, P], c_int),
+    "gca_hidden_init": ([c_uint64, c_int, c_int, c_int, c_int, P, P, P, P, P, P, P, P], c_int),
     "gca_ds_count_draws": ([P, c_int, c_int, c_int, c_int, c_int, c_int, P, P], c_int),
     "gca_ds_step": ([P, P, c_int, c_int, c_int, c_int, c_int, c_int, P, P, P, c_uint64, P, c_int, P, P], c_int),
 }

@@ -102,6 +102,13 @@ class CAEnv(ABC, _EnvBase):
         raise NotImplementedError
 
     def count_cells(self, grid=None):
-        """Returns dict of cell counts (ca_env.py:94-99). Device grids are counted on the GPU."""
+        """Dict of cell counts (ca_env.py:94-99). A device tensor is counted where it lives (torch.unique on the
+        GPU, only the per-value totals come back); a host grid as in the reference. The forest-fire envs
+        override this with the fused gca_count_cells kernel."""
         grid = self.grid if grid is None else grid
+        if hasattr(grid, "is_cuda") and grid.is_cuda:
+            import torch
+
+            values, counts = torch.unique(grid, return_counts=True)
+            return Counter(dict(zip(values.cpu().tolist(), counts.cpu().tolist())))
         return Counter(np.asarray(grid).ravel().tolist())

@@ -58,10 +58,11 @@ class EpisodeStats:
 
 
 def all_gather_stats(done, ret, length, group=None):
-    """One all_gather of a packed [done u8 | ret f32 | len i32] byte buffer (9 bytes per env)."""
+    """One all_gather of a packed [ret f32 | len i32 | done u8] byte buffer (9 bytes per env; the 4-byte
+    fields first so their views stay aligned for any env count)."""
     E = done.numel()
-    payload = torch.cat([done.reshape(-1).to(torch.uint8), ret.reshape(-1).to(torch.float32).view(torch.uint8),
-                         length.reshape(-1).to(torch.int32).view(torch.uint8)])
+    payload = torch.cat([ret.reshape(-1).to(torch.float32).view(torch.uint8),
+                         length.reshape(-1).to(torch.int32).view(torch.uint8), done.reshape(-1).to(torch.uint8)])
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
         parts = [payload]
     else:
@@ -69,7 +70,7 @@ def all_gather_stats(done, ret, length, group=None):
         dist.all_gather(parts, payload, group=group)
     dones, rets, lens = [], [], []
     for part in parts:
-        dones.append(part[:E])
-        rets.append(part[E:5 * E].view(torch.float32))
-        lens.append(part[5 * E:9 * E].view(torch.int32))
+        rets.append(part[:4 * E].view(torch.float32))
+        lens.append(part[4 * E:8 * E].view(torch.int32))
+        dones.append(part[8 * E:9 * E])
     return torch.cat(dones), torch.cat(rets), torch.cat(lens)

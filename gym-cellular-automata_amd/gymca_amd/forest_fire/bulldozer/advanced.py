@@ -7,12 +7,24 @@ Reference: advanced_bulldozer.py:63-1133 (JAX, vmap over num_envs). One env step
                       new-grid tree/fire counts fused
     gca_advenv_post   wind change (:442-451), f32 time accumulation (repeat_ca_jax.py:191-198),
                       MoveJax/ModifyJax (move_modify_jax.py:39-157), time_step/is_night
-                      (advanced_bulldozer.py:1116-1127), reward -(f/(t+f+1e-8)) and done (:597-633)
+                      (advanced_bulldozer.py:1116-1127), reward -(f/(t+f+1e-8)) and done (:597-633),
+                      info["steps_elapsed"] / info["reward_accumulated"] (:396-397)
 
-and `conditional_reset` (:422-518) re-injects the initial state of finished envs with
-gca_reset_where. observation="rgb" adds the reference's observation (gca_adv_observation:
-RGB f32 (E, H, W, 3) of the extension/blur/visibility pipeline, :988-1101, and the reset
-observation :401-411); observation="grid" (default) returns the true u8 grid instead.
+Reference batched API (the drop-in surface, advanced_bulldozer.py:332-518):
+
+    obs, info = env.reset()
+    obs, reward, terminated, truncated, info = env.stateless_step(action, obs, info)
+    obs, reward, terminated, truncated, info = env.conditional_reset(step_tuple, action)
+
+obs = (rgb f32 (E, H, W, 3), context) with context = {"per_env_context": {...}, "shared_context": {...},
+"position": (E, 2), "time": (E,)} — the reference's key sets (:109-129). The tensors are device views of
+the env's own HBM state: the JAX env threads state through obs/info functionally, here the state stays
+resident and `stateless_step` adopts whatever obs/info it is handed (a tensor that IS the env's buffer costs
+nothing; any other value — an older obs, a host array — is copied in). Returned tensors stay valid until the
+env's next step (they are the buffers the next step writes), as in other device-resident vector envs.
+observation="rgb" (default, the reference's) renders gca_adv_observation: RGB f32 of the
+extension/blur/visibility pipeline (:988-1101) and the reset observation (:401-411);
+observation="grid" returns the true u8 grid instead (cheaper; not the reference's obs).
 
 Device layout per env: grid u8 (ping-pong), fire_age i16 (ping-pong), vegetation /
 density / dousing u8, the slopes in the antisymmetric edge layout f32 [4][H][W]
@@ -28,6 +40,7 @@ import numpy as np
 
 from ... import _device as dev
 from ..._lib import AdvEnvParams, call
+from ..._seeding import env_integers
 from ..operators.ca_alexandridis import alex_constants, make_alex_params
 from .bulldozer import ACTION_SETS, bulldozer_timings
 from .init_utils import altitude_plan, device_altitude, get_winds, init_density, init_vegetation
@@ -38,7 +51,7 @@ class AdvancedForestFireBulldozerEnv:
     def __init__(self, nrows, ncols, key=0, num_envs=8, speed_move=0.12, speed_act=0.03, speed_multiplier=1.0,
                  pos_bull=None, pos_fire=None, t_move=None, t_shoot=None, t_any=0.001, p_tree=0.90, p_empty=0.10,
                  use_hidden=True, middle_fire=False, enable_extensions=False, device=None, env_offset=0,
-                 hidden_rng=None, slope_layout="auto", observation="grid", pinecones=False, tile_skip=False):
+                 hidden_rng=None, slope_layout="auto", observation="rgb", pinecones=False, tile_skip=False):
         import torch
 
         self.device = dev.require_device(device)
@@ -50,8 +63,8 @@ class AdvancedForestFireBulldozerEnv:
         self.middle_fire = middle_fire
         self._empty, self._tree, self._fire = 0, 1, 2
         self._p_tree_init, self._p_empty_init = p_tree, p_empty
-        self._pos_bull = pos_bull
-        self._pos_fire = pos_fire
+        self._pos_bull = _per_env_bull(pos_bull, self.num_envs)
+        self._pos_fire = _per_env_fire(pos_fire, self.num_envs)
         self._p_fire = 0.00033
         self._p_tree = 0.0  # advanced_bulldozer.py:209
         self._p_wind_change = 0.06
@@ -123,9 +136,15 @@ class AdvancedForestFireBulldozerEnv:
         self.done = torch.zeros(E, dtype=torch.uint8, **kw)
         self.steps_elapsed = torch.zeros(E, dtype=torch.float32, **kw)
         self.reward_accumulated = torch.zeros(E, dtype=torch.float32, **kw)
+        self.truncated = torch.zeros(E, dtype=torch.bool, **kw)  # the reference never truncates (:392)
+        self._winds_dev = torch.as_tensor(self._winds, device=self.device)
         self._initial = None
         if observation not in ("grid", "rgb"):
             raise ValueError("observation must be 'grid' or 'rgb'")
+        if observation == "rgb" and H != W:
+            # the reference's reset observation broadcasts the raw (H, W) grid against (W, W)-shaped colour
+            # arrays (advanced_bulldozer.py:405-409), so it only exists for square grids
+            raise ValueError("observation='rgb' (the reference's) needs a square grid; use observation='grid'")
         self.observation = observation
         self.enable_extensions = bool(enable_extensions)
         # MDP(should_transform_grid = transform_grid and enable_extensions, ...) (advanced_bulldozer.py:293-302)
@@ -139,11 +158,29 @@ class AdvancedForestFireBulldozerEnv:
         """density / vegetation / altitude -> slope, once per env instance like the reference's
         constructor (advanced_bulldozer.py:182-204). With use_hidden the layers come from the
         init_utils restatement, which consumes `rng` (default: the global np.random state, as the
-        reference does) draw for draw; altitude's arithmetic and get_slope run on the device."""
+        reference does) draw for draw; altitude's arithmetic and get_slope run on the device.
+        rng="philox" draws the same recipe on the device instead (gca_hidden_init)."""
         E, H, W = self.num_envs, self.nrows, self.ncols
         st = dev.stream_ptr(self.device)
         self.altitude = None
-        if self.use_hidden:
+        if self.use_hidden and isinstance(rng, str):
+            if rng != "philox":
+                raise ValueError("hidden_rng: None, a numpy random source, or 'philox'")
+            import torch
+
+            # the same recipe drawn on the device, keyed by the global env id (gca_hidden_init): milliseconds
+            # instead of seconds at E = 4096, and shard-invariant; not the reference's np.random stream
+            self.altitude = torch.empty((E, H, W), dtype=torch.float64, device=self.device)
+            nh = torch.empty(E, dtype=torch.int32, device=self.device)
+            ns = torch.empty(E, dtype=torch.int32, device=self.device)
+            hills = torch.empty((E, 10, 4), dtype=torch.float64, device=self.device)
+            slopes = torch.empty((E, 8, 5), dtype=torch.float64, device=self.device)
+            call("gca_hidden_init", self.key & (2**64 - 1), self.env_offset, E, H, W, dev.ptr(self.vegetation),
+                 dev.ptr(self.density), dev.ptr(self.altitude), dev.ptr(nh), dev.ptr(hills), dev.ptr(ns),
+                 dev.ptr(slopes), st)
+            call("gca_alex_altitude_apply", dev.ptr(self.altitude), E, H, W, dev.ptr(nh), dev.ptr(hills), dev.ptr(ns),
+                 dev.ptr(slopes), st)
+        elif self.use_hidden:
             import torch
 
             den = init_density(H, W, E, rng)
@@ -203,13 +240,12 @@ class AdvancedForestFireBulldozerEnv:
              dev.stream_ptr(self.device))
         return out
 
-    def reset(self, seed=None, options=None):
-        """Initial state of advanced_bulldozer.py:650-743 for every env."""
+    def reset(self, *, seed=None, options=None):
+        """Initial state of advanced_bulldozer.py:650-743 for every env; returns (obs, info) like :401-420."""
         import torch
 
         E, H, W = self.num_envs, self.nrows, self.ncols
         st = dev.stream_ptr(self.device)
-        rng = np.random.default_rng(self.key if seed is None else seed)
         # grid iid over {EMPTY, TREE} (p_empty, p_tree), two fires with age (N + N//2) * 2 (:650-688)
         cdf = torch.tensor([self._p_empty_init, self._p_empty_init + self._p_tree_init, 1.0], dtype=torch.float32,
                            device=self.device)
@@ -218,19 +254,30 @@ class AdvancedForestFireBulldozerEnv:
         call("gca_fill_categorical", dev.ptr(self.grid[0]), H * W, E, self.env_offset,
              (self.key if seed is None else int(seed)) & (2**64 - 1), dev.ptr(cdf), dev.ptr(vals), 3, st)
         self.age[0].zero_()
+        # fires: per env the cells of pos_fire[env] (default (3N/4, N/4) and its left neighbour, or the middle),
+        # age (N + N//2) * 2 (:664-688). Negative indices wrap as in the reference's .at[].set; a cell outside
+        # the grid raises here (JAX would drop the update silently)
         if self._pos_fire is not None:
-            r, c = self._pos_fire
-        elif self.middle_fire:
-            r, c = H // 2, W // 2
+            fires = self._pos_fire
         else:
-            r, c = 3 * H // 4, W // 4
-        age0 = (H + H // 2) * 2
-        for cc in (c, c - 1):
-            self.grid[0][:, r, cc] = self._fire
-            self.age[0][:, r, cc] = age0
-        br, bc = (int(H * 0.15), int(W * 0.85)) if self._pos_bull is None else self._pos_bull
-        self.pos[:, 0], self.pos[:, 1] = br, bc
-        wi = rng.integers(0, 8, size=E) if self.use_hidden else np.zeros(E)
+            r, c = (H // 2, W // 2) if self.middle_fire else (3 * H // 4, W // 4)
+            fires = [[(r, c), (r, c - 1)]] * E
+        ei = np.array([e for e in range(E) for _ in fires[e]], np.int64)
+        rc = np.array([p for e in range(E) for p in fires[e]], np.int64).reshape(-1, 2)
+        if rc.size and ((rc[:, 0] < -H).any() or (rc[:, 0] >= H).any() or (rc[:, 1] < -W).any() or
+                        (rc[:, 1] >= W).any()):
+            raise ValueError("pos_fire holds a cell outside the grid")
+        rc = rc % np.array([H, W])
+        idx = (torch.as_tensor(ei, device=self.device), torch.as_tensor(rc[:, 0], device=self.device),
+               torch.as_tensor(rc[:, 1], device=self.device))
+        self.grid[0].index_put_(idx, torch.tensor(self._fire, dtype=torch.uint8, device=self.device))
+        self.age[0].index_put_(idx, torch.tensor((H + H // 2) * 2, dtype=torch.int16, device=self.device))
+        # bulldozer: pos_bull[env], default (int(0.15 N), int(0.85 N)) (:690-700)
+        bull = self._pos_bull if self._pos_bull is not None else [(int(H * 0.15), int(W * 0.85))] * E
+        self.pos.copy_(torch.as_tensor(np.asarray(bull, np.int32).reshape(E, 2), device=self.device))
+        # initial wind index per env (:703-709), keyed by the global env id (shard-invariant)
+        wi = (env_integers(self.key if seed is None else int(seed), self.env_offset, E, 0x57494E44, 0, 8)
+              if self.use_hidden else np.zeros(E))
         self.wind_index.copy_(torch.as_tensor(wi.astype(np.int32), device=self.device))
         self.dousing.zero_()
         if self.dous_bits is not None:
@@ -242,6 +289,7 @@ class AdvancedForestFireBulldozerEnv:
         self.is_night.zero_()
         self.rng_step.zero_()
         self.done.zero_()
+        self.reward.zero_()
         self.steps_elapsed.zero_()
         self.reward_accumulated.zero_()
         call("gca_count_cells", dev.ptr(self.grid[0]), E, H, W, self._empty, self._tree, self._fire,
@@ -250,7 +298,7 @@ class AdvancedForestFireBulldozerEnv:
                              wind_index=self.wind_index.clone(), counts=self.counts.clone())
         if self.rgb is not None:  # the reference's reset observation (advanced_bulldozer.py:405-409)
             call("gca_adv_observation", self.obs_params, 1, E, H, W, dev.ptr(self.grid[0]), dev.ptr(self.dousing),
-                 dev.ptr(self.pos), dev.ptr(self.is_night), None, None, 0, dev.ptr(self.rgb), None, st)
+                 dev.ptr(self.pos), dev.ptr(self.is_night), None, None, 0, dev.ptr(self.rgb), None, None, st)
         return self._obs(), self._info()
 
     def set_state(self, grid=None, fire_age=None, vegetation=None, density=None, wind_index=None, dousing=None,
@@ -294,14 +342,83 @@ class AdvancedForestFireBulldozerEnv:
         call("gca_count_cells", dev.ptr(self.grid[self.cur]), E, H, W, self._empty, self._tree, self._fire,
              dev.ptr(self.counts), st)
 
-    # ------------------------------------------------------------------ step
+    # ------------------------------------------------------------------ obs / info (reference layout)
+    def _context(self):
+        """The reference's context dict (advanced_bulldozer.py:109-129, :711-743) over device views.
+        Layout differences: "key" is the per-env Philox step counter (the JAX PRNG key's role), "slope" the
+        step's slope layout (edge values (E, 4, H, W), coalesced when packed, or p_slope planes (E, 8, H, W)
+        instead of (E, H, W, 3, 3)), "fire_age" i16, "true_grid" / "dousing_count" / "vegetation" / "density"
+        u8; "altitude" is None without hidden layers."""
+        per_env = {"wind_index": self.wind_index, "density": self.density, "vegetation": self.vegetation,
+                   "altitude": self.altitude, "slope": self.slope_data, "fire_age": self.age[self.cur],
+                   "key": self.rng_step, "is_night": self.is_night, "true_grid": self.grid[self.cur],
+                   "time_step": self.time_step, "dousing_count": self.dousing}
+        shared = {"winds": self._winds_dev, "p_fire": self._p_fire, "p_tree": self._p_tree,
+                  "p_wind_change": self._p_wind_change, "day_length": self._day_length}
+        return {"per_env_context": per_env, "shared_context": shared, "position": self.pos, "time": self.accu}
+
     def _obs(self):
-        ctx = {"per_env_context": {"wind_index": self.wind_index, "fire_age": self.age[self.cur],
-                                   "dousing_count": self.dousing, "vegetation": self.vegetation,
-                                   "density": self.density, "time_step": self.time_step, "is_night": self.is_night,
-                                   "true_grid": self.grid[self.cur], "rng_step": self.rng_step},
-               "position": self.pos, "time": self.accu}
-        return (self.rgb if self.rgb is not None else self.grid[self.cur]), ctx
+        return (self.rgb if self.rgb is not None else self.grid[self.cur]), self._context()
+
+    def _info(self):
+        return {"reward": self.reward, "terminated": self.done.bool(), "TimeLimit.truncated": self.truncated,
+                "steps_elapsed": self.steps_elapsed, "reward_accumulated": self.reward_accumulated}
+
+    def _adopt(self, obs=None, info=None):
+        """Make the env's device state the one `obs` / `info` describe (the functional reference threads state
+        through them, :332-399). Values that are this env's own buffers are skipped (zero cost in the usual
+        loop that passes back what the last call returned); anything else is copied in."""
+        import torch
+
+        touched = set()
+
+        def load(x, buf, name):
+            if x is None:
+                return
+            if dev.is_device_tensor(x) and x.data_ptr() == buf.data_ptr() and x.dtype == buf.dtype \
+                    and tuple(x.shape) == tuple(buf.shape):
+                return
+            src = x if dev.is_device_tensor(x) else torch.as_tensor(np.asarray(x))
+            if tuple(src.shape) != tuple(buf.shape):
+                raise ValueError(f"{name}: shape {tuple(src.shape)} does not match the env's {tuple(buf.shape)}")
+            buf.copy_(src.to(device=self.device, dtype=buf.dtype))
+            touched.add(name)
+
+        if obs is not None:
+            ctx = obs[1]
+            pe = ctx.get("per_env_context", {})
+            load(pe.get("true_grid"), self.grid[self.cur], "true_grid")
+            load(pe.get("fire_age"), self.age[self.cur], "fire_age")
+            load(pe.get("dousing_count"), self.dousing, "dousing_count")
+            load(pe.get("vegetation"), self.vegetation, "vegetation")
+            load(pe.get("density"), self.density, "density")
+            load(pe.get("wind_index"), self.wind_index, "wind_index")
+            load(pe.get("is_night"), self.is_night, "is_night")
+            load(pe.get("time_step"), self.time_step, "time_step")
+            load(pe.get("key"), self.rng_step, "key")
+            load(ctx.get("position"), self.pos, "position")
+            load(ctx.get("time"), self.accu, "time")
+            if obs[0] is not None and self.rgb is not None:
+                load(obs[0], self.rgb, "rgb")
+        if info is not None:
+            load(info.get("steps_elapsed"), self.steps_elapsed, "steps_elapsed")
+            load(info.get("reward_accumulated"), self.reward_accumulated, "reward_accumulated")
+            load(info.get("reward"), self.reward, "reward")
+        if {"vegetation", "density", "dousing_count"} & touched:
+            if self.dous_bits is not None and bool((self.dousing > 1).any()):
+                raise ValueError("the packed layout stores dousing counts as bits: values must be 0/1")
+            self._pack_layers()
+        if "true_grid" in touched:
+            if self.act is not None:
+                self.act.fill_(1)
+            call("gca_count_cells", dev.ptr(self.grid[self.cur]), self.num_envs, self.nrows, self.ncols, self._empty,
+                 self._tree, self._fire, dev.ptr(self.counts), dev.stream_ptr(self.device))
+
+    def _full_action(self, action):
+        import torch
+
+        full = action if dev.is_device_tensor(action) else torch.as_tensor(np.asarray(action), device=self.device)
+        return full.to(device=self.device, dtype=torch.int32).reshape(self.num_envs, -1).contiguous()
 
     def render_observation(self, action=None, channels=None):
         """The step observation (gca_adv_observation mode 0) of the current state into self.rgb; `action`
@@ -311,12 +428,9 @@ class AdvancedForestFireBulldozerEnv:
         a = action if (action is not None and action.shape[-1] >= 3) else None
         call("gca_adv_observation", self.obs_params, 0, E, H, W, dev.ptr(self.grid[self.cur]), dev.ptr(self.dousing),
              dev.ptr(self.pos), dev.ptr(self.is_night), dev.ptr(self.time_step), dev.ptr(a),
-             0 if a is None else int(a.shape[-1]), dev.ptr(self.rgb), dev.ptr(channels), dev.stream_ptr(self.device))
+             0 if a is None else int(a.shape[-1]), dev.ptr(self.rgb), dev.ptr(channels), None,
+             dev.stream_ptr(self.device))
         return self.rgb
-
-    def _info(self):
-        return {"reward": self.reward, "terminated": self.done.bool(), "steps_elapsed": self.steps_elapsed,
-                "reward_accumulated": self.reward_accumulated}
 
     def ca_step(self):
         """The CA step alone (RepeatCAJax's one step) for every env; swaps the ping-pong buffers."""
@@ -348,40 +462,63 @@ class AdvancedForestFireBulldozerEnv:
                  dev.ptr(None if self.act is None else self.act[b]), dev.stream_ptr(self.device))
 
     def step(self, action):
-        """action: (E, 2) or (E, 3) ints (move, shoot[, extension]); device tensor or numpy."""
-        import torch
-
-        E, H, W = self.num_envs, self.nrows, self.ncols
-        full = action if dev.is_device_tensor(action) else torch.as_tensor(np.asarray(action), device=self.device)
-        full = full.to(torch.int32).reshape(E, -1).contiguous()
-        a = full[:, :2].contiguous()
+        """Gymnasium-style step of every env: action (E, 2) or (E, 3) ints (move, shoot[, extension choice]),
+        device tensor or numpy. Returns (obs, reward, terminated, truncated, info) like stateless_step."""
+        full = self._full_action(action)
         self.ca_step()
-        self.post_step(a)
+        self.post_step(full[:, :2].contiguous(), stats=True)
         if self.rgb is not None:
             self.render_observation(full)
-        self.steps_elapsed += 1
-        self.reward_accumulated += self.reward
-        terminated = self.done.bool()
-        return self._obs(), self.reward, terminated, torch.zeros_like(terminated), self._info()
+        return self._obs(), self.reward, self.done.bool(), self.truncated, self._info()
 
-    stateless_step = step
+    def stateless_step(self, action, obs=None, info=None):
+        """The reference's batched step (advanced_bulldozer.py:332-399): action (E, 3) = (move, shoot, extension
+        choice); obs / info as returned by reset / the previous call (their state is adopted, see _adopt).
+        Returns (obs, reward, terminated, truncated, info) with info["reward" / "terminated" /
+        "TimeLimit.truncated" / "steps_elapsed" / "reward_accumulated"]."""
+        self._adopt(obs, info)
+        return self.step(action)
 
-    def post_step(self, action2):
-        """gca_advenv_post for (E, 2) int32 device actions: wind change, time, Move/Modify, reward, done."""
+    def post_step(self, action2, stats=False):
+        """gca_advenv_post for (E, 2) int32 device actions: wind change, time, Move/Modify, reward, done
+        (+ the info episode statistics steps_elapsed / reward_accumulated when `stats`)."""
         E, H, W = self.num_envs, self.nrows, self.ncols
         call("gca_advenv_post", self.env_params, dev.ptr(action2), dev.ptr(self.pos), dev.ptr(self.accu),
              dev.ptr(self.wind_index), dev.ptr(self.time_step), dev.ptr(self.is_night), dev.ptr(self.dousing),
              dev.ptr(self.dous_bits), H, W, dev.ptr(self.counts), dev.ptr(self.rng_step), dev.ptr(self.reward),
-             dev.ptr(self.done), E, dev.stream_ptr(self.device))
+             dev.ptr(self.done), dev.ptr(self.steps_elapsed if stats else None),
+             dev.ptr(self.reward_accumulated if stats else None), E, dev.stream_ptr(self.device))
 
-    def conditional_reset(self):
-        """Re-inject the initial state of terminated envs (:422-518); time_step/is_night are kept."""
+    def conditional_reset(self, step_tuple=None, action=None, *, seed=None, options=None):
+        """The reference's conditional_reset (advanced_bulldozer.py:422-518): envs whose `terminated` flag is
+        set in `step_tuple` (default: this env's last step) get their initial state back — grid, fire ages,
+        dousing, wind index, position, time, RNG key; time_step / is_night are kept (:497-507) — and their
+        observation is rebuilt from the initial grid with `action`'s extension choice and the step's (pre-reset)
+        per-env context (:455-481). info steps_elapsed / reward_accumulated restart at 0 for them, the reward
+        is the award of the resulting grid and `terminated` comes back all False (:509-516). Every launch exits
+        at once for live envs, so nothing syncs with the host (the reference's lax.cond, :518-523). `seed` and
+        `options` are accepted for signature parity; like the reference's traced initial_state they change
+        nothing."""
         import torch
 
         E, H, W = self.num_envs, self.nrows, self.ncols
+        st = dev.stream_ptr(self.device)
+        if step_tuple is not None:
+            obs, _, terminated, _, info = step_tuple
+            self._adopt(obs, info)
+            if terminated is not None:
+                t = terminated if dev.is_device_tensor(terminated) else torch.as_tensor(np.asarray(terminated))
+                if not (dev.is_device_tensor(t) and t.data_ptr() == self.done.data_ptr()):
+                    self.done.copy_(t.reshape(E).to(device=self.device, dtype=torch.uint8))
         init = self._initial
-        done = self.done.clone()
-        mask = done.bool()
+        mask = self.done.bool()
+        if self.rgb is not None:
+            # the re-injected envs' observation: initial grid and position, the step's dousing and is_night
+            # (no day/night undo: the context is the post-step one), action's extension choice; others untouched
+            a = None if action is None else self._full_action(action)
+            call("gca_adv_observation", self.obs_params, 0, E, H, W, dev.ptr(init["grid"]), dev.ptr(self.dousing),
+                 dev.ptr(init["pos"]), dev.ptr(self.is_night), None, dev.ptr(a), 0 if a is None else int(a.shape[-1]),
+                 dev.ptr(self.rgb), None, dev.ptr(self.done), st)
         self.steps_elapsed.masked_fill_(mask, 0)
         self.reward_accumulated.masked_fill_(mask, 0.0)
         self.rng_step.masked_fill_(mask, 0)  # the reference re-injects the initial JAX key
@@ -393,6 +530,36 @@ class AdvancedForestFireBulldozerEnv:
         call("gca_reset_where", dev.ptr(self.done), E, H, W, dev.ptr(self.grid[self.cur]), dev.ptr(init["grid"]),
              dev.ptr(self.age[self.cur]), dev.ptr(init["age"]), dev.ptr(self.dousing), None,
              dev.ptr(self.dous_bits), dev.ptr(self.pos),
-             dev.ptr(init["pos"]), dev.ptr(self.accu), dev.ptr(self.wind_index), dev.ptr(init["wind_index"]),
-             dev.stream_ptr(self.device))
-        return self._obs(), self.reward, self.done.bool(), torch.zeros_like(mask), self._info()
+             dev.ptr(init["pos"]), dev.ptr(self.accu), dev.ptr(self.wind_index), dev.ptr(init["wind_index"]), st)
+        return self._obs(), self.reward, self.done.bool(), self.truncated, self._info()
+
+
+def _per_env_bull(pos_bull, E):
+    """pos_bull as the reference takes it — a list of E (row, col) pairs (advanced_bulldozer.py:690-700) — or one
+    (row, col) pair for every env; None = the default. Returns a list of E pairs or None."""
+    if pos_bull is None:
+        return None
+    a = np.asarray(pos_bull, dtype=np.int64)
+    if a.shape == (2,):
+        return [tuple(int(v) for v in a)] * E
+    if a.shape == (E, 2):
+        return [tuple(int(v) for v in row) for row in a]
+    raise ValueError(f"pos_bull must be (row, col) or a list of {E} (row, col) pairs, got shape {a.shape}")
+
+
+def _per_env_fire(pos_fire, E):
+    """pos_fire as the reference takes it — per env a list of (row, col) fire cells (advanced_bulldozer.py:664-688:
+    [[(r, c), (r, c - 1)], ...]) — or one (row, col) pair, meaning (r, c) and (r, c - 1) in every env (the
+    reference's default pattern). None = the default. Returns a list of E lists of pairs or None."""
+    if pos_fire is None:
+        return None
+    if np.asarray(pos_fire, dtype=object).shape == (2,) and all(np.isscalar(v) for v in pos_fire):
+        r, c = int(pos_fire[0]), int(pos_fire[1])
+        return [[(r, c), (r, c - 1)]] * E
+    if len(pos_fire) != E:
+        raise ValueError(f"pos_fire must be (row, col) or a list of {E} per-env lists of (row, col) cells")
+    out = []
+    for cells in pos_fire:
+        a = np.asarray(cells, dtype=np.int64).reshape(-1, 2) if len(cells) else np.zeros((0, 2), np.int64)
+        out.append([tuple(int(v) for v in row) for row in a])
+    return out

@@ -74,13 +74,17 @@ class BatchedForestFireBulldozerEnv:
         return torch.where(self.parity.bool()[:, None, None], self.buf[1], self.buf[0])
 
     def reset(self, seed=None, grids=None, positions=None):
-        """Reset all envs. Initial distribution of bulldozer.py:233-275, drawn with Philox
-        (grid) and a numpy Generator seeded from `seed` (fire / bulldozer noise)."""
+        """Reset all envs. Initial distribution of bulldozer.py:233-275: the grid from Philox per cell, the fire /
+        bulldozer noise from per-env draws keyed by the global env id (_seeding), so a sharded env reproduces the
+        unsharded one env for env."""
         import torch
+
+        from ..._seeding import env_integers
 
         E, H, W = self.num_envs, self.nrows, self.ncols
         st = dev.stream_ptr(self.device)
-        rng = np.random.default_rng(self.seed_value if seed is None else seed)
+        s = self.seed_value if seed is None else int(seed)
+        noise = lambda tag, n: env_integers(s, self.env_offset, E, tag, 0, max(1, int(n / 12)))
         if grids is not None:
             self.buf[0].copy_(dev.to_device(np.asarray(grids).reshape(E, H, W).astype(np.uint8), torch.uint8,
                                             self.device))
@@ -91,16 +95,15 @@ class BatchedForestFireBulldozerEnv:
             call("gca_fill_categorical", dev.ptr(self.buf[0]), H * W, E, self.env_offset,
                  (self.seed_value if seed is None else int(seed)) & (2**64 - 1), dev.ptr(cdf), dev.ptr(vals), 3, st)
             # one FIRE around the lower-left quadrant, noise in [0, N/12) (bulldozer.py:221-253)
-            fr = 3 * H // 4 + rng.integers(0, max(1, int(H / 12)), E)
-            fc = W // 4 + rng.integers(0, max(1, int(W / 12)), E)
+            fr = 3 * H // 4 + noise(1, H)
+            fc = W // 4 + noise(2, W)
             idx = torch.arange(E, device=self.device)
             self.buf[0][idx, torch.as_tensor(fr, device=self.device), torch.as_tensor(fc, device=self.device)] = \
                 self._fire
         if positions is not None:
             pos = np.asarray(positions).reshape(E, 2)
         else:
-            pos = np.stack([H // 4 + rng.integers(0, max(1, int(H / 12)), E),
-                            3 * W // 4 + rng.integers(0, max(1, int(W / 12)), E)], axis=1)
+            pos = np.stack([H // 4 + noise(3, H), 3 * W // 4 + noise(4, W)], axis=1)
         self.pos.copy_(torch.as_tensor(pos.astype(np.int32), device=self.device))
         self.parity.zero_()
         self.accu.zero_()

@@ -1,8 +1,11 @@
 """ForestFireBulldozerEnv — single-env drop-in (reference bulldozer.py:21-400).
 
 Same constructor, spaces, operator graph (MDP = RepeatCA(WindyForestFire) then
-MoveModify) and Gymnasium step/reset. The CA, Move/Modify and the reward/done cell
-counts run on the GPU. The batched, device-resident version of the same MDP is
+MoveModify) and Gymnasium step/reset. The grid stays resident on the GPU between
+steps: the CA passes, Move/Modify (one fused launch) and ONE cell count per step (shared
+by _is_done and _award) run there; only the observation copy goes to the host
+(numpy int64 like the reference's obs; `obs_device=True` returns the device u8 grid
+instead and skips that copy). The batched version of the same MDP is
 `BatchedForestFireBulldozerEnv` (batched.py); that is the performance path.
 
 Deliberate difference: the reference crashes on its first CA step
@@ -96,9 +99,12 @@ class ForestFireBulldozerEnv(CAEnv):
         p_tree=0.90,
         p_empty=0.10,
         wind=DEFAULT_WIND,
+        obs_device=False,
         **kwargs,
     ):
         super().__init__(nrows, ncols, **kwargs)
+        self.obs_device = bool(obs_device)
+        self._counts = None  # this step's device count (Counter), shared by _is_done and _award
         self.title = "ForestFireBulldozer" + str(nrows) + "x" + str(ncols)
         self._shoots = {"shoot": 1, "none": 0}
         self._empty, self._tree, self._fire = 0, 3, 25
@@ -126,21 +132,58 @@ class ForestFireBulldozerEnv(CAEnv):
     def render(self, mode="human"):  # rendering is out of scope
         return None
 
+    # ------------------------------------------------------------------ device-resident state
+    def _to_device_grid(self):
+        """The env's grid as the device u8 tensor it lives in (a host array set by the caller is adopted)."""
+        import torch
+
+        if not dev.is_device_tensor(self.grid):
+            arr = np.asarray(self.grid)
+            if arr.size and (arr.min() < 0 or arr.max() > 255):
+                raise ValueError("cell values must fit the u8 device layout (0..255)")
+            self.grid = dev.to_device(arr.astype(np.uint8), torch.uint8, dev.require_device())
+        return self.grid
+
+    def _host_obs(self, obs):
+        grid, ctx = obs
+        if self.obs_device or not dev.is_device_tensor(grid):
+            return obs
+        return grid.cpu().numpy().astype(TYPE_INT), ctx
+
+    def step(self, action):
+        self._to_device_grid()
+        self.state = self.grid, self.context
+        self._counts = None  # Modify edits the grid in place: the count is per step, not per grid object
+        obs, reward, terminated, truncated, info = super().step(action)
+        return self._host_obs(obs), reward, terminated, truncated, info
+
+    def reset(self, *, seed=None, options=None):
+        _, info = super().reset(seed=seed, options=options)
+        self._to_device_grid()
+        self.state = self.grid, self.context
+        return self._host_obs(self.state), info
+
     def _award(self):
-        """-(f / (t + f)) (bulldozer.py:180-213); counts come from the device."""
-        counts = self.count_cells(self.grid)
+        """-(f / (t + f)) (bulldozer.py:180-213) from the step's one device count."""
+        counts = self._step_counts()
         t = counts[self._tree]
         f = counts[self._fire]
         return -(f / (t + f))
 
     def _is_done(self):
-        self.done = not bool(self.count_cells(self.grid)[self._fire])
+        self.done = not bool(self._step_counts()[self._fire])
+
+    def _step_counts(self):
+        """One gca_count_cells per step: _is_done and then _award read the same count of the same grid."""
+        if self._counts is None:
+            self._counts = self.count_cells(self.grid)
+        return self._counts
 
     def _report(self):
         return {"hit": self.modify.hit}
 
     def count_cells(self, grid=None):
-        """Counts of EMPTY/TREE/FIRE computed by gca_count_cells on the device."""
+        """Counts of EMPTY/TREE/FIRE computed by gca_count_cells on the device (host grids are uploaded)."""
         import torch
         from collections import Counter
 

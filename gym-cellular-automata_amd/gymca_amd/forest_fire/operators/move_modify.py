@@ -127,6 +127,7 @@ class MoveModify(Operator):
         self.suboperators = move, modify
         self.move = move
         self.modify = modify
+        self._fused = None
         if self.action_space is None:
             if self.move.action_space is not None and self.move.action_space is not None:
                 self.action_space = Tuple((self.move.action_space, self.move.action_space))
@@ -137,6 +138,17 @@ class MoveModify(Operator):
 
     def update(self, grid, subactions, position):
         move_action, modify_action = subactions
+        if type(self.move) is Move and type(self.modify) is Modify:
+            # both are this package's device operators: Move then Modify in ONE gca_move_modify launch
+            # (the kernel moves first and modifies at the new position, move_modify.py:128-134)
+            if self._fused is None:
+                d = {"up": self.move.up_set, "down": self.move.down_set, "left": self.move.left_set,
+                     "right": self.move.right_set}
+                self._fused = make_params(d, self.modify.effects)
+            shoot = bool(modify_action)
+            position, hit = _run(self._fused, grid, (int(move_action), int(shoot)), position, with_grid=shoot)
+            self.modify.hit = hit
+            return grid, position
         grid, position = self.move(grid, move_action, position)
         grid, position = self.modify(grid, modify_action, position)
         return grid, position

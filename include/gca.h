@@ -41,6 +41,8 @@ extern "C" {
 #define GCA_TAG_DS_CELL    0x44534345u /* 'DSCE' : Drossel-Schwabl per-cell draws     */
 #define GCA_TAG_PINE       0x50494E45u /* 'PINE' (+1+m): pinecone count / pinecone m  */
 #define GCA_TAG_PINE_AGE   0x50494E41u /* 'PINA' : age of a pinecone-ignited cell     */
+#define GCA_TAG_HIDDEN     0x48494444u /* 'HIDD' : per-env hidden-layer plan (patches, hills, slopes) */
+#define GCA_TAG_HIDDEN_CELL 0x48494443u /* 'HIDC' : per-cell hidden-layer draws          */
 
 /* ------------------------------------------------------------------ generic */
 
@@ -221,6 +223,22 @@ int gca_alex_slope_from_altitude(const double* altitude, float* p_slope, float* 
 int gca_alex_altitude_apply(double* altitude, int E, int H, int W, const int32_t* n_hills, const double* hills,
                             const int32_t* n_slopes, const double* slopes, void* stream);
 
+/* Hidden layers drawn on the device (init_utils.py:10-116's recipe, Philox draws keyed by the GLOBAL env id,
+ * so sharded runs draw what the unsharded run draws; not the reference's np.random stream — the envs'
+ * hidden_rng="philox" mode). Per env (counter (slot, env_offset + e, 0, GCA_TAG_HIDDEN)):
+ *   vegetation / density: randint(4, 8) patches (centre randint(0, R) x randint(0, C), size randint(3, max(4,
+ *     R//2)) x randint(3, max(4, C//2)), value randint(1, 6)), later patches over earlier ones, uncovered cells
+ *     randint(1, 4);
+ *   altitude: noise uniform(0, 5) per cell into `altitude`, and the hills / slopes plan of
+ *     gca_alex_altitude_apply (randint(6, 10) hills: centre, radius randint(2, max(3, min(R, C)//4)), height
+ *     uniform(2, 6); randint(4, 8) slopes: start randint(0, max(1, R-4)) x randint(0, max(1, C-4)), width
+ *     randint(3, max(4, C//4)), height randint(3, max(4, R//4)), height_diff uniform(1, 4)).
+ * Per cell (counter (r * W + c, env_offset + e, 0, GCA_TAG_HIDDEN_CELL)): word 0 -> vegetation fill, word 1
+ * -> density fill, words 2:3 -> noise. Follow with gca_alex_altitude_apply to finish the altitude.          */
+int gca_hidden_init(uint64_t seed, int env_offset, int E, int H, int W, uint8_t* vegetation, uint8_t* density,
+                    double* altitude, int32_t* n_hills, double* hills, int32_t* n_slopes, double* slopes,
+                    void* stream);
+
 /* Pinecone spotting (ca_alexandridis_jax.py:229-319, the scatter :400-420 — disabled in the reference's
  * live path, enabled in our env / operator with pinecones=True), after gca_alex_step* on its output:
  * every FIRE cell of grid_in throws n = min(Poisson(1), max_pinecones) pinecones in direction d (uniform
@@ -264,11 +282,13 @@ typedef struct {
 /* After gca_alex_step: wind change (repeat: ca_alexandridis_jax.py:442-451), time
  * accumulation (repeat_ca_jax.py:191-198, f32), MoveJax, ModifyJax (dousing[r][c] = 1
  * if shoot==1), time_step += 1, is_night toggle, reward = -(f/(t+f+1e-8)) f32,
- * done = no fire, rng_step += 1. dous_bits (nullable): the packed layout's dousing bits, set with dousing. */
+ * done = no fire, rng_step += 1. dous_bits (nullable): the packed layout's dousing bits, set with dousing.
+ * steps_elapsed / reward_accumulated (nullable, f32 [E]): stateless_step's episode statistics
+ * info["steps_elapsed"] += 1, info["reward_accumulated"] += reward (advanced_bulldozer.py:396-397).    */
 int gca_advenv_post(const gca_advenv_params* p, const int32_t* action, int32_t* pos, float* accu,
                     int32_t* wind_index, int32_t* time_step, int32_t* is_night, uint8_t* dousing, uint16_t* dous_bits,
-                    int H, int W, const int32_t* counts, uint32_t* rng_step, float* reward, uint8_t* done, int E,
-                    void* stream);
+                    int H, int W, const int32_t* counts, uint32_t* rng_step, float* reward, uint8_t* done,
+                    float* steps_elapsed, float* reward_accumulated, int E, void* stream);
 
 /* conditional_reset (advanced_bulldozer.py:422-518): envs with done[e] copy their
  * initial grid/age/dousing/position/time/wind_index (and clear done); dous_bits (nullable, packed layout)
@@ -307,10 +327,13 @@ typedef struct {
  *   action_stride < 3 = no extension active.
  * mode 1 (reset, :401-411): the reference applies grid_to_rgb_with_extensions to the raw (H, W)
  *   grid; its broadcasting gives rgb[r][c] = colour(grid[c][k]) with k = 3 + the first row holding a
- *   positive value in columns 3.. (clamped), or k = 0 — reproduced as is (square grids only).   */
+ *   positive value in columns 3.. (clamped), or k = 0 — reproduced as is (square grids only).
+ * env_mask (nullable, u8 [E]): only envs with env_mask[e] != 0 are rendered, the others' rgb/channels
+ *   are left untouched — conditional_reset's per-env jnp.where(terminated, new obs, old obs) (:464-481). */
 int gca_adv_observation(const gca_obs_params* p, int mode, int E, int H, int W, const uint8_t* grid,
                         const uint8_t* dousing, const int32_t* pos, const int32_t* is_night, const int32_t* time_step,
-                        const int32_t* action, int action_stride, float* rgb, uint8_t* channels, void* stream);
+                        const int32_t* action, int action_stride, float* rgb, uint8_t* channels,
+                        const uint8_t* env_mask, void* stream);
 
 /* Synthetic inputs for benches/tests (Philox, GCA_TAG_INIT / GCA_TAG_ACTION). */
 int gca_fill_categorical(uint8_t* out, int64_t n_per_env, int E, int env_offset, uint64_t seed,

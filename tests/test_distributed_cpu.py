@@ -79,3 +79,40 @@ def test_sharded_philox_streams_equal_unsharded():
         b.step(act[2:])
     for e in range(E):
         assert np.array_equal(full.grids[e], (a.grids + b.grids)[e])
+
+
+def test_all_gather_stats_any_env_count():
+    """The packed payload keeps its f32 / i32 views aligned for env counts that are not multiples of 4."""
+    for E in (1, 3, 5, 1023):
+        done = (torch.arange(E) % 2).to(torch.uint8)
+        d, r, ln = all_gather_stats(done, -torch.arange(E, dtype=torch.float32), torch.arange(E, dtype=torch.int32))
+        assert torch.equal(d, done) and torch.equal(r, -torch.arange(E, dtype=torch.float32))
+        assert torch.equal(ln, torch.arange(E, dtype=torch.int32))
+
+
+def _bench(*argv, env=None):
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    e = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    e.update(env or {})
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), *argv], capture_output=True, text=True,
+                       timeout=240, env=e, cwd=root)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    return p.returncode, (json.loads(lines[-1]) if lines else None), p.stderr
+
+
+def test_bench_gpus2_dry_run_spawns_two_gloo_ranks():
+    """`python bench.py --gpus 2 --dry-run` starts two ranks itself (no torchrun in front), each takes its env
+    shard and the episode-stats all-gather the bench uses returns every rank's envs in order."""
+    rc, out, err = _bench("--gpus", "2", "--dry-run", "--envs", "7")
+    assert rc == 0, err[-2000:]
+    assert out["n_gpus"] == 2 and out["backend"] == "gloo" and out["gather_ok"]
+    assert [(r["rank"], r["env_offset"], r["envs"]) for r in out["ranks"]] == [(0, 0, 7), (1, 7, 7)]
+
+
+def test_bench_refuses_a_world_size_mismatch():
+    rc, out, err = _bench("--gpus", "2", env={"WORLD_SIZE": "1", "RANK": "0"})
+    assert rc != 0 and out is None and "WORLD_SIZE=1" in err

@@ -318,3 +318,94 @@ def test_classic_philox_bit_exact_vs_c_oracle(device, H, W):
         assert np.array_equal(g2.cpu().numpy(), go) and np.array_equal(a2.cpu().numpy(), ao), f"step {step}"
         assert np.array_equal(counts.cpu().numpy(), co)
         grid, age, g_d, a_d = go, ao, g2, a2
+
+
+def test_philox_and_injected_modes_share_probabilities(device):
+    """The Philox-mode kernel (MODE 1 = MODE 0 + the debug probability output) and the injected-draw kernel
+    (MODE 2) compute bit-identical per-direction burn probabilities on the same state: the draw mode changes
+    only how the uniforms are compared, never p_d."""
+    E, H, W = 3, 96, 80
+    case = make_case(E, H, W, 57, p_tree=0.1)
+    p = params(H, 0.1)
+    *_, po_philox, _ = run_kernel(device, p, case, rng_step=np.full(E, 3, np.uint32), probs=True)
+    *_, po_inj, _ = run_kernel(device, p, case, inj=case["draws"], probs=True)
+    assert np.array_equal(po_philox.view(np.uint32), po_inj.view(np.uint32))
+
+
+def test_packed_fast_kernel_burn_law_chi_square(device):
+    """The timed kernel (gca_alex_step_packed: MODE 0, FAST, edge slopes, packed layout) against the
+    reference's burn law. The reference ignites a TREE iff some burning neighbour d has u_d < p_d with
+    independent uniforms (ca_alexandridis_jax.py:379-383), i.e. with probability 1 - prod_d (1 - clamp01(p_d));
+    the kernel draws one uniform against that product. 32 envs x 256^2 mid-episode states (hidden layers,
+    random dousing) give ~0.6M TREE cells with 1..8 burning neighbours and 0 < law < 1, plus cells with every p_d <= 0
+    (dousing) and a few with p_d > 1 (steep slopes); 48 launches
+    with distinct Philox steps. Expected p_d: the independent float64 evaluation
+    oracle.alexandridis_ref.burn_probability_f64. Cells binned by expected law (40 quantile bins): sum over
+    bins of (observed - expected)^2 / variance ~ chi2(40); the test fails above chi2.isf(1e-6, 40) (false-alarm
+    rate 1e-6). Cells with every p_d <= 0 must never ignite, cells with some p_d >= 1.001 always."""
+    import torch
+    from scipy.stats import chi2
+
+    from gymca_amd import _device as dev
+    from gymca_amd._lib import call
+    from gymca_amd.forest_fire.bulldozer import AdvancedForestFireBulldozerEnv
+    from gymca_amd.forest_fire.bulldozer.init_utils import get_slope
+
+    E, N, T = 32, 256, 48
+    env = AdvancedForestFireBulldozerEnv(N, N, key=606, num_envs=E, use_hidden=True, hidden_rng="philox",
+                                         device=device, observation="grid", slope_layout="packed")
+    env.reset()
+    rng = np.random.default_rng(12)
+    grid = rng.choice(np.array([0, 1, 2], np.uint8), size=(E, N, N), p=[0.1, 0.6, 0.3])
+    age = np.where(grid == 2, 500, 0).astype(np.int16)
+    dous = (rng.random((E, N, N)) < 0.03).astype(np.uint8)
+    widx = rng.integers(0, 8, E).astype(np.int32)
+    env.set_state(grid=grid, fire_age=age, dousing=dous, wind_index=widx)
+    g_in = env.grid[env.cur].clone()
+    age0 = env.age[env.cur].clone()
+    g_out = torch.empty_like(g_in)
+    age_buf = torch.empty((E, N, N), dtype=torch.int16, device=device)
+    counts = torch.zeros((E, 3), dtype=torch.int32, device=device)
+    burned = torch.zeros((E, N, N), dtype=torch.int32, device=device)
+    st = dev.stream_ptr(device)
+    for t in range(T):
+        age_buf.copy_(age0)  # the packed step updates ages in place
+        rs = torch.full((E,), 1000 + t, dtype=torch.int32, device=device)
+        call("gca_alex_step_packed", env.alex_params, E, N, N, dev.ptr(g_in), dev.ptr(g_out), dev.ptr(age_buf),
+             dev.ptr(age_buf), dev.ptr(env.vd), dev.ptr(env.dous_bits), dev.ptr(env.slope_data), dev.ptr(env.wind_index),
+             dev.ptr(rs), dev.ptr(counts), None, None, st)
+        burned += ((g_out == 2) & (g_in == 1)).to(torch.int32)
+    burned = burned.cpu().numpy()
+    slope = get_slope(env.altitude.cpu().numpy(), N, N, E).astype(np.float32)
+    veg, den = env.vegetation.cpu().numpy(), env.density.cpu().numpy()
+    W8 = winds()[:, 0]
+    C = ref.constants(N)
+    laws, obs, always, never = [], [], [], []
+    for e in range(E):
+        pd = ref.burn_probability_f64(grid[e], veg[e], den[e], W8[widx[e]], slope[e], dous[e], C).reshape(N, N, 9)
+        nbf = (ref._nbhd(grid[e].astype(np.float32), 1) == 2).reshape(N, N, 9)
+        nbf[..., 4] = False
+        cand = (grid[e] == 1) & nbf.any(-1)
+        q = np.where(nbf, 1.0 - np.clip(pd, 0.0, 1.0), 1.0).prod(-1)
+        law = 1.0 - q
+        hi = (np.where(nbf, pd, -np.inf).max(-1) >= 1.001) & cand
+        lo = (np.where(nbf, pd, -np.inf).max(-1) <= 0.0) & cand
+        mid = cand & ~hi & ~lo & (law > 0) & (law < 1)
+        laws.append(law[mid])
+        obs.append(burned[e][mid])
+        always.append(burned[e][hi])
+        never.append(burned[e][lo])
+        assert np.all(burned[e][~cand] == 0)  # no burning neighbour (or not a TREE): never ignites
+    laws, obs = np.concatenate(laws), np.concatenate(obs)
+    always, never = np.concatenate(always), np.concatenate(never)
+    assert laws.size > 500_000 and always.size >= 10 and never.size > 100
+    assert np.all(always == T) and np.all(never == 0)
+    assert laws.min() < 0.01 and laws.max() > 0.99  # the bins span the whole (0, 1) range
+    B = 40
+    edges = np.quantile(laws, np.linspace(0, 1, B + 1))
+    b = np.clip(np.searchsorted(edges, laws, side="right") - 1, 0, B - 1)
+    o = np.bincount(b, weights=obs, minlength=B)
+    ex = T * np.bincount(b, weights=laws, minlength=B)
+    var = T * np.bincount(b, weights=laws * (1 - laws), minlength=B)
+    stat = float(((o - ex) ** 2 / var).sum())
+    assert stat < chi2.isf(1e-6, B), (stat, chi2.isf(1e-6, B))

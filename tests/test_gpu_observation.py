@@ -29,7 +29,7 @@ def run(device, params, mode, grid, dous, pos, night, time_step=None, action=Non
     rgb = torch.full((E, H, W, 3), -1.0, dtype=torch.float32, device=device)
     ch = torch.full((E, H, W, 5), 255, dtype=torch.uint8, device=device) if channels else None
     call("gca_adv_observation", params, mode, E, H, W, dev.ptr(g), dev.ptr(d), dev.ptr(p_), dev.ptr(n_), dev.ptr(ts),
-         dev.ptr(a), 0 if a is None else int(a.shape[-1]), dev.ptr(rgb), dev.ptr(ch), dev.stream_ptr())
+         dev.ptr(a), 0 if a is None else int(a.shape[-1]), dev.ptr(rgb), dev.ptr(ch), None, dev.stream_ptr())
     return rgb.cpu().numpy(), None if ch is None else ch.cpu().numpy()
 
 

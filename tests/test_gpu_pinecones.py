@@ -60,7 +60,8 @@ def test_env_pinecones_ignite_only_trees(device):
     from gymca_amd.forest_fire.bulldozer import AdvancedForestFireBulldozerEnv
 
     E, N = 2, 256
-    envs = [AdvancedForestFireBulldozerEnv(N, N, key=9, num_envs=E, use_hidden=False, device=device, pinecones=pc)
+    envs = [AdvancedForestFireBulldozerEnv(N, N, key=9, num_envs=E, use_hidden=False, device=device, pinecones=pc,
+                                           observation="grid")
             for pc in (True, False)]
     case = make_case(E, N, N, 41, hidden=False)
     for env in envs:

@@ -92,7 +92,7 @@ def test_philox_dirmask_matches_oracle(device):
             assert got[e] == owindy.dir_mask(wind[e], owindy.philox_roll(seed, 100 + e, step))
 
 
-@pytest.mark.parametrize("N,E,steps", [(32, 6, 120), (64, 4, 80), (256, 3, 60), (40, 5, 60)])
+@pytest.mark.parametrize("N,E,steps", [(32, 6, 120), (64, 4, 80), (256, 3, 60), (40, 5, 60), (512, 3, 160)])
 def test_batched_bulldozer_env_matches_oracle(device, N, E, steps):
     from gymca_amd.forest_fire.bulldozer import BatchedForestFireBulldozerEnv
 
@@ -197,13 +197,15 @@ def test_reference_repeat_ca_two_steps(device):
     assert np.array_equal(observed, g2) and accu == 0.0
 
 
-def test_full_size_windy_properties(device):
-    """BASELINE config 2 size (1024 x 256^2) through the batched env's forced CA step:
-    FIRE -> EMPTY, EMPTY stays, counts add up, and a sampled env equals the oracle."""
+@pytest.mark.parametrize("N", [256, 512])  # BASELINE config 2 / config 5's per-GPU shard
+def test_full_size_windy_properties(device, N):
+    """BASELINE config 2 size (1024 x 256^2) and config 5's per-GPU shard (1024 x 512^2, 268 MB per buffer)
+    through the batched env's forced CA step: FIRE -> EMPTY, EMPTY stays, TREE stays or burns, and sampled
+    envs equal the oracle."""
     torch = _torch()
     from gymca_amd.forest_fire.bulldozer import BatchedForestFireBulldozerEnv
 
-    E, N = 1024, 256
+    E = 1024
     env = BatchedForestFireBulldozerEnv(E, N, N, device=device, seed=3, p_tree=0.6, p_empty=0.1)
     env.reset()
     # dense variant: sprinkle fire
@@ -260,3 +262,39 @@ def test_batched_env_graph_replay_equals_eager(device):
     for name in ("pos", "accu", "rng_step", "done", "counts", "reward"):
         ta, tb = getattr(a, name), getattr(b, name)
         assert torch.equal(torch.nan_to_num(ta), torch.nan_to_num(tb)), name
+
+
+def _windy_pair(device, E, N, seed):
+    from gymca_amd.forest_fire.bulldozer import BatchedForestFireBulldozerEnv
+
+    full = BatchedForestFireBulldozerEnv(E, N, N, device=device, seed=seed)
+    shards = [BatchedForestFireBulldozerEnv(E // 2, N, N, device=device, seed=seed, env_offset=k * (E // 2))
+              for k in range(2)]
+    return full, shards
+
+
+@pytest.mark.parametrize("N", [64, 512])
+def test_sharded_windy_env_equals_unsharded(device, N):
+    """two env objects owning envs [0, E/2) and [E/2, E) (env_offset) step bit-identically to one
+    env owning all E — reset draws, CA rolls and device actions are keyed by the global env id."""
+    import torch
+
+    from gymca_amd import _device as dev
+    from gymca_amd._lib import call
+
+    E = 8
+    full, shards = _windy_pair(device, E, N, seed=23)
+    for env in (full, *shards):
+        env.reset(seed=9)
+    acts = [torch.zeros((env.num_envs, 2), dtype=torch.int32, device=device) for env in (full, *shards)]
+    for s in range(40):
+        for env, a in zip((full, *shards), acts):
+            call("gca_random_actions", dev.ptr(a), env.num_envs, env.env_offset, 31, dev.ptr(env.rng_step),
+                 dev.stream_ptr(device))
+            env.step(a)
+        assert torch.equal(torch.cat([acts[1], acts[2]]), acts[0])
+        assert torch.equal(torch.cat([shards[0].grids(), shards[1].grids()]), full.grids()), f"step {s}"
+        for name in ("pos", "accu", "rng_step", "done", "counts", "hit"):
+            assert torch.equal(torch.cat([getattr(shards[0], name), getattr(shards[1], name)]), getattr(full, name))
+        assert torch.equal(torch.nan_to_num(torch.cat([shards[0].reward, shards[1].reward])),
+                           torch.nan_to_num(full.reward))
