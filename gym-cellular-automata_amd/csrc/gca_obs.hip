@@ -31,7 +31,13 @@
 #define GCA_OBS_WAVE 1  // wave-local RGB transposition (each wave stores its own 3 KiB), no barriers per round; 0: block-wide (r01p A/B: 0.713 vs 0.722 ms)
 #endif
 #ifndef GCA_OBS_RB
-#define GCA_OBS_RB 32  // rows per workgroup (r01o A/B at W = 256: 8 / 16 / 32 / 48 / 64 rows -> 0.90 / 0.76 / 0.72 / 0.84 / 0.89 ms)
+#define GCA_OBS_RB 16  // rows per workgroup (r02f A/B at W = 256 with the wave-local transposition: 8 / 12 / 16 / 32 rows -> 0.84 / 0.70 / 0.64 / 0.70 ms; r01o block-wide: 16 / 32 -> 0.76 / 0.72)
+#endif
+#ifndef GCA_OBS_PRE
+#define GCA_OBS_PRE 5  // staged 16-B chunks per thread issued before the display scan (W = 256, 32 rows: 4.1 needed)
+#endif
+#ifndef GCA_OBS_BATCH
+#define GCA_OBS_BATCH 1  // full rounds: 3 LDS reads, one wait, 3 stores (A/B hook)
 #endif
 #ifndef GCA_OBS_NT
 #define GCA_OBS_NT 1  // non-temporal RGB stores (r01i A/B: 1.07 vs 1.10 ms per 4096 x 256^2)
@@ -139,7 +145,34 @@ __global__ __launch_bounds__(256) void adv_observation_kernel(gca_obs_params p, 
     for (int i = 0; i < p.n_ext; ++i) k.need_blur |= ((k.on >> i) & 1u) && !p.ext_skip_blur[i];
     const int nch = 3 + p.n_ext;
 
-    // ---- display selection (see the header comment in include/gca.h)
+    // ---- staging loads first (W % 16 == 0, 16-B aligned: the production shape): up to GCA_OBS_PRE 16-B
+    //      chunks per thread go to registers now and to LDS after the display scan, so the scan's loads and
+    //      these overlap instead of queueing one HBM round trip behind the other at the head of every block
+    const bool stage_all = (W & 3) == 0;  // the 4-cells-per-thread path reads both arrays from LDS
+    const bool do_stage = mode == 0 && (stage_all || k.need_blur);
+    const bool al16 = ((((uintptr_t)grid) | ((uintptr_t)dousing)) & 15u) == 0;
+    const bool fast16 = do_stage && (W & 15) == 0 && al16;
+    const int w16 = W >> 4;
+    const int ng16 = (rows + 2) * w16, nd16 = du ? rows * w16 : 0;
+    const int nst = fast16 ? ng16 + nd16 : 0;
+    // byte offset of staged 16-B chunk idx (grid rows r0-1 .. r0+rows edge-clamped, then the dousing rows)
+    // from g; the dousing array is addressed relative to the grid (same env, same layout)
+    const int64_t dgap = du ? (int64_t)(du - g) : 0;
+    auto src16 = [&](int idx) -> int64_t {
+        const int lr = idx / w16, cq = idx - lr * w16;
+        const int r = min(max(r0 - 1 + lr, 0), H - 1);
+        return idx < ng16 ? (int64_t)r * W + 16 * cq : dgap + (int64_t)r0 * W + 16 * (int64_t)(idx - ng16);
+    };
+    uint4 pre[GCA_OBS_PRE];
+#pragma unroll
+    for (int j = 0; j < GCA_OBS_PRE; ++j) {  // unconditional loads of clamped chunks: pre stays in VGPRs
+        const int idx = min((int)threadIdx.x + 256 * j, max(nst - 1, 0));
+        pre[j] = nst ? *reinterpret_cast<const uint4*>(g + src16(idx)) : make_uint4(0u, 0u, 0u, 0u);
+    }
+
+    // ---- display selection (see the header comment in include/gca.h). Every wave scans on its own (the
+    //      result is a function of the grid alone, so all waves agree): no workgroup barrier per scanned row
+    const int lane = (int)threadIdx.x & 63;
     int sel = -1;     // mode 0: -1 = base channel, else the extension channel shown everywhere
     int col_sel = 0;  // mode 1: column of the raw grid shown
     if (mode == 0 && k.on) {
@@ -148,20 +181,32 @@ __global__ __launch_bounds__(256) void adv_observation_kernel(gca_obs_params p, 
         int fv = -1;
         for (int r = 0; r < H && fv < 0; ++r) {
             int any = 0;
-            for (int c = threadIdx.x; c < W; c += blockDim.x) {
-                const int raw = g[(int64_t)r * W + c];
-                const int bl = scan_blur ? blur_at(g, H, W, r, c) : raw;
-                for (int i = 0; i < p.n_ext; ++i) any |= ext_value(p, k, i, raw, bl) > 0;
+            if ((W & 3) == 0) {
+                for (int c4 = 4 * lane; c4 < W; c4 += 256) {
+                    const uint32_t w = *reinterpret_cast<const uint32_t*>(g + (int64_t)r * W + c4);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int raw = (int)((w >> (8 * j)) & 0xFFu);
+                        const int bl = scan_blur ? blur_at(g, H, W, r, c4 + j) : raw;
+                        for (int i = 0; i < p.n_ext; ++i) any |= ext_value(p, k, i, raw, bl) > 0;
+                    }
+                }
+            } else {
+                for (int c = lane; c < W; c += 64) {
+                    const int raw = g[(int64_t)r * W + c];
+                    const int bl = scan_blur ? blur_at(g, H, W, r, c) : raw;
+                    for (int i = 0; i < p.n_ext; ++i) any |= ext_value(p, k, i, raw, bl) > 0;
+                }
             }
-            if (__syncthreads_or(any)) fv = r;
+            if (__ballot(any) != 0ull) fv = r;
         }
         if (fv >= 0) sel = min(fv, p.n_ext - 1);
     } else if (mode == 1 && W > 3) {
         int fv = -1;
         for (int r = 0; r < H && fv < 0; ++r) {
             int any = 0;
-            for (int c = 3 + threadIdx.x; c < W; c += blockDim.x) any |= g[(int64_t)r * W + c] > 0;
-            if (__syncthreads_or(any)) fv = r;
+            for (int c = 3 + lane; c < W; c += 64) any |= g[(int64_t)r * W + c] > 0;
+            if (__ballot(any) != 0ull) fv = r;
         }
         col_sel = fv >= 0 ? 3 + min(fv, W - 4) : 0;
     }
@@ -177,9 +222,7 @@ __global__ __launch_bounds__(256) void adv_observation_kernel(gca_obs_params p, 
     }
 
     // ---- stage grid rows [r0 - 1, r0 + rows] (clamped: edge padding, for the blur) and the block's dousing
-    //      rows in LDS, every load issued before any is used: the render rounds below then read LDS only
-    //      and never wait on HBM between their stores
-    const bool stage_all = (W & 3) == 0;  // the 4-cells-per-thread path reads both arrays from LDS
+    //      rows in LDS: the render rounds below then read LDS only and never wait on HBM between their stores
     // the block's 12 colours (kind x dousing 0 / 1 / >= 2) in LDS: the render rounds then index LDS instead of
     // the kernel arguments (a per-lane index into them is a vector memory load, whose wait would also drain
     // the previous round's stores)
@@ -189,21 +232,16 @@ __global__ __launch_bounds__(256) void adv_observation_kernel(gca_obs_params p, 
         render_kind(p, c3, (int)threadIdx.x / 3, (int)threadIdx.x % 3, k.night);
         COLT[threadIdx.x] = make_float4(c3[0], c3[1], c3[2], 0.0f);
     }
-    if (stage_all || k.need_blur) {
-        const bool al16 = ((((uintptr_t)grid) | ((uintptr_t)dousing)) & 15u) == 0;
-        if ((W & 15) == 0 && al16) {
-            const int w16 = W >> 4;
-            const int ng = (rows + 2) * w16, nd = du ? rows * w16 : 0;
-            for (int idx = threadIdx.x; idx < ng + nd; idx += blockDim.x) {
-                if (idx < ng) {
-                    const int lr = idx / w16, cq = idx - lr * w16;
-                    const int r = min(max(r0 - 1 + lr, 0), H - 1);
-                    reinterpret_cast<uint4*>(T)[lr * w16 + cq] = reinterpret_cast<const uint4*>(g + (int64_t)r * W)[cq];
-                } else {
-                    const int j = idx - ng;
-                    reinterpret_cast<uint4*>(D)[j] = reinterpret_cast<const uint4*>(du + (int64_t)r0 * W)[j];
-                }
+    if (do_stage) {
+        if (fast16) {
+#pragma unroll
+            for (int j = 0; j < GCA_OBS_PRE; ++j) {
+                const int idx = (int)threadIdx.x + 256 * j;
+                if (idx < ng16 + nd16) reinterpret_cast<uint4*>(idx < ng16 ? T : D - 16 * ng16)[idx] = pre[j];
             }
+            for (int idx = (int)threadIdx.x + 256 * GCA_OBS_PRE; idx < ng16 + nd16; idx += 256)
+                reinterpret_cast<uint4*>(idx < ng16 ? T : D - 16 * ng16)[idx] =
+                    *reinterpret_cast<const uint4*>(g + src16(idx));
         } else if (stage_all) {
             const int wq = W >> 2;
             const int ng = (rows + 2) * wq, nd = du ? rows * wq : 0;
@@ -223,8 +261,8 @@ __global__ __launch_bounds__(256) void adv_observation_kernel(gca_obs_params p, 
                 T[idx] = g[(int64_t)min(max(r0 - 1 + lr, 0), H - 1) * W + c];
             }
         }
-        __syncthreads();
     }
+    __syncthreads();
 
     auto values_of = [&](int raw, int bl, int* extv) -> int {
         const int base = p.should_transform ? transform(raw, bl, k.night, 0, 0) : raw;
@@ -303,13 +341,22 @@ __global__ __launch_bounds__(256) void adv_observation_kernel(gca_obs_params p, 
 #endif
             const int n4 = 3 * min(256, rows * wq - base_q);
             float4* dst = reinterpret_cast<float4*>(rgb + (e * HW + (int64_t)r0 * W + 4 * (int64_t)base_q) * 3);
+            typedef float f4v __attribute__((ext_vector_type(4)));
+            if (GCA_OBS_BATCH && GCA_OBS_WAVE && GCA_OBS_NT && n4 == 768) {
+                // a full round (all but a block's ragged last one): the three LDS reads issue back to back, one
+                // wait, then the three 1-KiB stores — not read / wait / store three times over
+                const int q0 = 192 * ((int)threadIdx.x >> 6) + ((int)threadIdx.x & 63);
+                const float4 v0 = OUT4[q0], v1 = OUT4[q0 + 64], v2 = OUT4[q0 + 128];
+                __builtin_nontemporal_store((f4v){v0.x, v0.y, v0.z, v0.w}, reinterpret_cast<f4v*>(dst + q0));
+                __builtin_nontemporal_store((f4v){v1.x, v1.y, v1.z, v1.w}, reinterpret_cast<f4v*>(dst + q0 + 64));
+                __builtin_nontemporal_store((f4v){v2.x, v2.y, v2.z, v2.w}, reinterpret_cast<f4v*>(dst + q0 + 128));
+            } else
 #pragma unroll
             for (int j = 0; j < 3; ++j) {
                 const int q4 = GCA_OBS_WAVE ? 192 * ((int)threadIdx.x >> 6) + ((int)threadIdx.x & 63) + 64 * j
                                             : (int)threadIdx.x + 256 * j;
                 if (q4 < n4) {
 #if GCA_OBS_NT
-                    typedef float f4v __attribute__((ext_vector_type(4)));
                     const float4 v = OUT4[q4];
                     __builtin_nontemporal_store((f4v){v.x, v.y, v.z, v.w}, reinterpret_cast<f4v*>(dst + q4));
 #else
