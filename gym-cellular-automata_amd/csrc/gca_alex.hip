@@ -148,7 +148,7 @@ template <class T, class S> __device__ __forceinline__ T bitcast_(S s) {
 template <int R, int MODE, bool FAST, bool ES, bool PK = false>
 __global__ __launch_bounds__(256, GCA_ALEX_WGS) void alex_step_kernel(
     gca_alex_params p, int H, int W, int tiles_r, int tiles_c, const uint8_t* __restrict__ grid_in,
-    uint8_t* __restrict__ grid_out, const int16_t* __restrict__ age_in, int16_t* __restrict__ age_out,
+    uint8_t* __restrict__ grid_out, const int16_t* age_in, int16_t* age_out,  // no __restrict__: PK updates in place
     const uint8_t* __restrict__ veg, const uint8_t* __restrict__ den, const uint8_t* __restrict__ dousing,
     const float* __restrict__ p_slope, const int32_t* __restrict__ wind_index, const uint32_t* __restrict__ rng_step,
     const float* __restrict__ inj_burn, const float* __restrict__ inj_grow, const int32_t* __restrict__ inj_age,

@@ -1,8 +1,9 @@
-"""RepeatCA — drop-in for the reference combinator (repeat_ca.py:11-45).
+"""RepeatCA: advance a CA by whole units of accumulated time (drop-in for repeat_ca.py:11-45).
 
-Host control logic only (it calls arbitrary Python timing callables): the CA it
-repeats runs on the device. The batched envs do the same bookkeeping in
-gca_bulldozer_pre (one lane per env).
+Each call adds the time of the action plus the time of the state to the carried fraction and runs the
+wrapped CA once per whole unit reached; the remainder is carried in the context as a float64 0-d array.
+Host control logic only (it calls user-supplied timing callables); the CA it drives runs on the device.
+The batched envs do the same bookkeeping per env in gca_bulldozer_pre (one lane per env).
 """
 import math
 from typing import Callable
@@ -20,19 +21,16 @@ class RepeatCA(Operator):
 
     def __init__(self, cellular_automaton, t_acting: Callable, t_perception: Callable, *args, **kwargs):
         super().__init__(*args, **kwargs)
-        self.t_acting = t_acting
-        self.t_perception = t_perception
         self.ca = cellular_automaton
-        self.suboperators = (self.ca,)
-        self.deterministic = self.ca.deterministic
+        self.t_acting, self.t_perception = t_acting, t_perception
+        self.suboperators = (cellular_automaton,)
+        self.deterministic = cellular_automaton.deterministic
 
     def update(self, grid, action, context):
-        ca_params, accu_time = context
-        time_action = self.t_acting(action)
-        time_state = self.t_perception((grid, context))
-        time_taken = time_action + time_state
-        accu_time += time_taken
-        accu_time, repeats = math.modf(accu_time)
-        for _ in range(int(repeats)):
+        ca_params, carried = context
+        # (action time + state time) first, then onto the carried fraction: the reference's f64 rounding order
+        elapsed = self.t_acting(action) + self.t_perception((grid, context))
+        fraction, whole = math.modf(carried + elapsed)
+        for _ in range(int(whole)):
             grid, ca_params = self.ca(grid, action, ca_params)
-        return grid, (ca_params, np.array(accu_time, dtype=TYPE_BOX))
+        return grid, (ca_params, np.array(fraction, dtype=TYPE_BOX))
