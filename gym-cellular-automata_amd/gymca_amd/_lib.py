@@ -27,6 +27,11 @@ TAG_HIDDEN = 0x48494444
 TAG_HIDDEN_CELL = 0x48494443
 GCA_PINE_MAX = 8
 GCA_PINE_CDF = 17
+TAG_PINEC = 0x50434C00
+TAG_PINEC_AGE = 0x50434C41
+GCA_PINEC_NMAX = 16
+GCA_PINEC_CDF = 48
+GCA_PINEC_LDS_MAX_HW = 327680
 
 
 class GCAError(RuntimeError):
@@ -89,6 +94,24 @@ class PineParams(ctypes.Structure):
         ("scale", c_float),
         ("veg1p", c_float * 6),
         ("den1p", c_float * 6),
+        ("age_lo", c_int32),
+        ("age_hi", c_int32),
+        ("seed", c_uint64),
+        ("env_offset", c_int32),
+        ("empty", c_int32),
+        ("tree", c_int32),
+        ("fire", c_int32),
+    ]
+
+
+class PineClassicParams(ctypes.Structure):
+    """gca_pine_classic_params (include/gca.h)."""
+
+    _fields_ = [
+        ("n_cdf", c_uint32 * GCA_PINEC_NMAX),
+        ("dx", c_int32 * 8),
+        ("dy", c_int32 * 8),
+        ("burn_thr", (c_uint32 * 6) * 6),
         ("age_lo", c_int32),
         ("age_hi", c_int32),
         ("seed", c_uint64),
@@ -165,6 +188,8 @@ _SIGNATURES = {
                          c_int),
     "gca_alex_edge_slope_from_altitude": ([P, P, c_int, c_int, c_int, P], c_int),
     "gca_alex_pinecones": ([POINTER(PineParams), c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, P], c_int),
+    "gca_alex_pinecones_classic": ([POINTER(PineClassicParams), c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P,
+                                    P], c_int),
     "gca_alex_step_packed": ([POINTER(AlexParams), c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, P, P, P], c_int),
     "gca_alex_pack_layers": ([P, P, P, P, P, c_int, c_int, c_int, P], c_int),
     "gca_alex_edge_slope_coalesce": ([P, P, c_int, c_int, c_int, P], c_int),

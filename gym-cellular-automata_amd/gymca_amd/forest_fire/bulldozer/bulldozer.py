@@ -192,8 +192,9 @@ class ForestFireBulldozerEnv(CAEnv):
         g = grid if dev.is_device_tensor(grid) else dev.to_device(np.asarray(grid).astype(np.uint8), torch.uint8,
                                                                    device)
         H, W = g.shape[-2:]
+        g = g.contiguous()  # keep the operand referenced until the count has run
         counts = torch.empty(3, dtype=torch.int32, device=device)
-        call("gca_count_cells", dev.ptr(g.contiguous()), 1, H, W, self._empty, self._tree, self._fire,
+        call("gca_count_cells", dev.ptr(g), 1, H, W, self._empty, self._tree, self._fire,
              dev.ptr(counts), dev.stream_ptr(device))
         c = counts.cpu().numpy().tolist()
         return Counter({v: n for v, n in zip((self._empty, self._tree, self._fire), c) if n})

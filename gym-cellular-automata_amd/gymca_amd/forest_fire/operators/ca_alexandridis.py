@@ -225,9 +225,9 @@ class PartiallyObservableForestFireJax(Operator):
 # p_h = 0.58 (:92-99), no heat kernel and no dousing; TREE with a FIRE neighbour burns iff any burning
 # neighbour's draw is below p_burn (:104-111), new fire age randint[4, 11) (:111); EMPTY -> TREE w.p.
 # p_tree (:171-177); FIRE: age -= 1 and EMPTY when it reaches 0 (:179-183); then the wind change
-# (:212-220). Pinecone spotting (:184-210) is not part of this operator (the
-# reference path draws from the global numpy RNG through `jax.numpy`, which has no `random`, so it
-# cannot run) — documented in DESIGN.md.
+# (:212-220). Pinecone spotting (:184-210) with the reference loop's skip list runs after the step as
+# gca_alex_pinecones_classic (pinecones=True, the default: the reference's update always spots; its own
+# path cannot run — it draws through `jax.numpy.random`, which does not exist).
 CLASSIC_VEG = {1: -0.3, 2: 0.0, 3: 0.3, 4: 0.6, 5: 1.0}  # :92
 CLASSIC_DEN = {1: -0.4, 2: 0.0, 3: 0.3, 4: 0.6, 5: 1.0}  # :93
 CLASSIC_P_H = 0.58  # :94
@@ -268,7 +268,9 @@ class PartiallyObservableForestFire(Operator):
     fire_age and wind_index are updated IN the context dict (the reference mutates it, :146-217) and
     `(new_grid, context)` is returned. Draws: Philox keyed by the operator's seed with a per-call step
     counter, or `draws=` with the reference's own arrays (burn (H,W,3,3) uniforms, grow (H,W), age
-    (H,W) ints, optional wind_u / wind_k) for an exact replay of the rule.
+    (H,W) ints, optional wind_u / wind_k) for an exact replay of the rule. Pinecones (`pinecones=True`)
+    always draw from Philox (seed `philox_seed`, env 0, the call's step counter): see
+    oracle/alexandridis_classic.decode_pinecone_draws for the reference arrays they correspond to.
     """
 
     grid_dependant = True
@@ -277,9 +279,10 @@ class PartiallyObservableForestFire(Operator):
 
     deterministic = False
 
-    def __init__(self, empty, tree, fire, *args, **kwargs):
+    def __init__(self, empty, tree, fire, *args, pinecones=True, **kwargs):
         super().__init__(*args, **kwargs)
         self.empty, self.tree, self.fire = empty, tree, fire
+        self.pinecones = bool(pinecones)
         dev.check_u8_codes((empty, tree, fire))
         if self.context_space is None:
             self.context_space = Box(0.0, 1.0, shape=(2,), dtype=TYPE_BOX)
@@ -330,6 +333,17 @@ class PartiallyObservableForestFire(Operator):
         call("gca_alex_step", p, 1, H, W, dev.ptr(grid_in), dev.ptr(grid_out), dev.ptr(age_in), dev.ptr(age_out),
              dev.ptr(veg), dev.ptr(den), dev.ptr(dous), dev.ptr(p_slope), dev.ptr(widx), dev.ptr(rng_step),
              dev.ptr(inj[0]), dev.ptr(inj[1]), dev.ptr(inj[2]), dev.ptr(probs), None, st)
+        if self.pinecones:  # :184-210, with the wind of the step (ft read at :137, before the change)
+            from ..._lib import GCA_PINEC_LDS_MAX_HW
+            from .pinecones import classic_thrust_tables, make_classic_pine_params
+
+            pp = make_classic_pine_params(self.philox_seed, self.empty, self.tree, self.fire)
+            tabs = torch.as_tensor(classic_thrust_tables(context["winds"]).view(np.int32), device=device)
+            scratch = None if H * W <= GCA_PINEC_LDS_MAX_HW else \
+                torch.empty(4 * ((H * W + 31) // 32), dtype=torch.int32, device=device)
+            call("gca_alex_pinecones_classic", pp, 1, H, W, dev.ptr(grid_in), dev.ptr(grid_out), dev.ptr(age_out),
+                 dev.ptr(veg), dev.ptr(den), dev.ptr(widx), dev.ptr(tabs), dev.ptr(rng_step), None, dev.ptr(scratch),
+                 st)
         call("gca_alex_wind_change", float(np.float32(context.get("p_wind_change", 0.0))), p.n_winds, p.seed, 0,
              dev.ptr(rng_step), dev.ptr(wu), dev.ptr(wk), dev.ptr(widx), 1, st)
         self._step += 1

@@ -43,6 +43,8 @@ extern "C" {
 #define GCA_TAG_PINE_AGE   0x50494E41u /* 'PINA' : age of a pinecone-ignited cell     */
 #define GCA_TAG_HIDDEN     0x48494444u /* 'HIDD' : per-env hidden-layer plan (patches, hills, slopes) */
 #define GCA_TAG_HIDDEN_CELL 0x48494443u /* 'HIDC' : per-cell hidden-layer draws          */
+#define GCA_TAG_PINEC      0x50434C00u /* 'PCL\0' (+1+m): classic pinecone count / pinecone m */
+#define GCA_TAG_PINEC_AGE  0x50434C41u /* 'PCLA' : age of a classic pinecone ignition        */
 
 /* ------------------------------------------------------------------ generic */
 
@@ -266,6 +268,41 @@ typedef struct {
 int gca_alex_pinecones(const gca_pine_params* p, int E, int H, int W, const uint8_t* grid_in, uint8_t* grid_out,
                        int16_t* age_out, const uint8_t* veg, const uint8_t* den, const int32_t* wind_index,
                        const uint32_t* s_cdf, const uint32_t* rng_step, int32_t* counts, uint8_t* act_tiles, void* stream);
+
+/* Classic pinecone spotting: PartiallyObservableForestFire.update's sequential skip-list pass
+ * (ca_alexandridis.py:184-210, sampling :35-69, ignition :113-133), after gca_alex_step (classic params) on
+ * its output. Every FIRE cell s of grid_in, in row-major order, throws N ~ Poisson(1) pinecones (tail folded at
+ * GCA_PINEC_NMAX); pinecone m has direction d uniform over 8 and integer thrust s_m = round(3 N(0,1) ft[lookup[d]])
+ * (:189-190, ft of the env's current wind), landing at (r + dx[d] s_m, c + dy[d] s_m). A landing inside the grid
+ * and not on s itself ignites its target - WHATEVER the target's state - iff u < 0.58 (1 + p_veg) (1 + p_den)
+ * of the target (burn_thr: u24 < thr), with a fresh age randint(4, 11). A target that ignites and comes LATER
+ * in the scan is skipped by the reference's loop (:151-152): when that target is itself a FIRE cell of grid_in it
+ * throws no pinecones. The device resolves that order dependence exactly: one workgroup per env iterates
+ * "s is active iff no active earlier source ignites it" to its fixed point (the dependence is a DAG in scan
+ * order), then applies the landings of the active sources. Ages are keyed by the target (the last of several
+ * ignitions of one target draws a fresh uniform age in the reference: the same law). counts (nullable):
+ * one count moves from the target's previous state to FIRE per ignited target.
+ * s_cdf [n_winds][8][GCA_PINEC_CDF] u32: per (wind, direction) t[0] = 2K, t[1..2K] thresholds of
+ * P(round(3 ft Z) <= -K + j) * 2^32. scratch: NULL when 16 * ceil(H W / 32) bytes fit one workgroup's LDS
+ * (H W <= 327680, e.g. 512 x 512), else E * 4 * ceil(H W / 32) u32 of device memory (the kernel clears it).
+ * Draws: Philox (lin, env, step, PINEC + 0) -> N, (lin, env, step, PINEC + 1 + m) -> s (word 0), u (word 1 >> 8),
+ * d (word 2 >> 29); (target lin, env, step, PINEC_AGE) word 0 -> age. */
+#define GCA_PINEC_NMAX 16
+#define GCA_PINEC_CDF 48
+#define GCA_PINEC_LDS_MAX_HW 327680
+typedef struct {
+    uint32_t n_cdf[GCA_PINEC_NMAX]; /* P(Poisson(1) <= j) * 2^32, j = 0..15 (N_p = poisson(), :37)              */
+    int32_t dx[8], dy[8];           /* dx_lookup / dy_lookup (:63-64)                                          */
+    uint32_t burn_thr[6][6];        /* [veg][den]: ceil(p * 2^24), p = 0.58 * (1 + p_veg) * (1 + p_den) in f64 */
+    int32_t age_lo, age_hi;         /* integers(4, 11) (:131)                                                  */
+    uint64_t seed;
+    int32_t env_offset;
+    int32_t empty, tree, fire;
+} gca_pine_classic_params;
+int gca_alex_pinecones_classic(const gca_pine_classic_params* p, int E, int H, int W, const uint8_t* grid_in,
+                               uint8_t* grid_out, int16_t* age_out, const uint8_t* veg, const uint8_t* den,
+                               const int32_t* wind_index, const uint32_t* s_cdf, const uint32_t* rng_step,
+                               int32_t* counts, uint32_t* scratch, void* stream);
 
 /* --------------------------------- AdvancedForestFireBulldozer env step (batched)
  * advanced_bulldozer.py:1103-1133 minus observations, + _award/_is_done :597-633.  */

@@ -141,3 +141,28 @@ def pinecones(params, grid_in, grid_out, age_out, veg, den, wind_index, s_cdf, r
     lib().oracle_alex_pinecones(ctypes.byref(o), E, H, W, _p(gi), _p(go), _p(ao), _p(veg), _p(den), _p(wi), _p(sc),
                                 _p(rs), _p(cn))
     return go, ao, cn
+
+
+class OraclePineClassicParams(ctypes.Structure):
+    _fields_ = [("n_cdf", ctypes.c_uint32 * 16), ("dx", ctypes.c_int32 * 8), ("dy", ctypes.c_int32 * 8),
+                ("burn_thr", (ctypes.c_uint32 * 6) * 6), ("age_lo", ctypes.c_int32), ("age_hi", ctypes.c_int32),
+                ("seed", ctypes.c_uint64), ("env_offset", ctypes.c_int32), ("empty", ctypes.c_int32),
+                ("tree", ctypes.c_int32), ("fire", ctypes.c_int32)]
+
+
+def pinecones_classic(params, grid_in, grid_out, age_out, veg, den, wind_index, s_cdf, rng_step=None, counts=None):
+    """oracle_alex_pinecones_classic (the literal sequential skip-list order) on copies; params: a
+    field-compatible struct (the product's PineClassicParams). Returns (grid_out, age_out, counts,
+    skipped_sources[E])."""
+    o = OraclePineClassicParams()
+    ctypes.memmove(ctypes.addressof(o), ctypes.addressof(params), ctypes.sizeof(o))
+    E, H, W = grid_in.shape
+    c = lambda a, t: np.ascontiguousarray(a, dtype=t)
+    gi, go, ao = c(grid_in, np.uint8), c(grid_out, np.uint8).copy(), c(age_out, np.int16).copy()
+    veg, den, wi, sc = c(veg, np.uint8), c(den, np.uint8), c(wind_index, np.int32), c(s_cdf, np.uint32)
+    rs = None if rng_step is None else c(rng_step, np.uint32)
+    cn = None if counts is None else c(counts, np.int32).copy()
+    skipped = np.zeros(E, dtype=np.int32)
+    lib().oracle_alex_pinecones_classic(ctypes.byref(o), E, H, W, _p(gi), _p(go), _p(ao), _p(veg), _p(den), _p(wi),
+                                        _p(sc), _p(rs), _p(cn), _p(skipped))
+    return go, ao, cn, skipped

@@ -329,3 +329,80 @@ void oracle_alex_pinecones(const oracle_pine_params* p, int E, int H, int W, con
         }
     }
 }
+
+/* ------------------------------------------------------------------ classic pinecone spotting
+ * The sequential skip-list loop of PartiallyObservableForestFire.update (ca_alexandridis.py:149-210) restricted
+ * to its pinecone part, on the output of the classic step: cells are visited in row-major order, a visited FIRE
+ * cell of grid_in throws its pinecones (the device's draw convention, gca_pine.hip), a landing inside the grid and
+ * not on the thrower ignites its target whatever its state (u24 < burn_thr), and an ignited target later in the
+ * order is put on the skip list (a skipped FIRE cell throws nothing). Ages of ignited targets: the target-keyed
+ * draw. The device resolves the same order dependence in parallel; this loop is the literal order. */
+#define PINEC_NMAX 16
+#define PINEC_CDF 48
+#define TAG_PINEC 0x50434C00u
+#define TAG_PINEC_AGE 0x50434C41u
+typedef struct {
+    uint32_t n_cdf[PINEC_NMAX];
+    int32_t dx[8], dy[8];
+    uint32_t burn_thr[6][6];
+    int32_t age_lo, age_hi;
+    uint64_t seed;
+    int32_t env_offset;
+    int32_t empty, tree, fire;
+} oracle_pine_classic_params;
+
+void oracle_alex_pinecones_classic(const oracle_pine_classic_params* p, int E, int H, int W, const uint8_t* grid_in,
+                                   uint8_t* grid_out, int16_t* age_out, const uint8_t* veg, const uint8_t* den,
+                                   const int32_t* wind_index, const uint32_t* s_cdf, const uint32_t* rng_step,
+                                   int32_t* counts, int32_t* n_skipped_sources) {
+    const long HW = (long)H * W;
+    const uint32_t k0 = (uint32_t)p->seed, k1 = (uint32_t)(p->seed >> 32);
+    uint8_t* skip = (uint8_t*)malloc((size_t)HW);
+    for (int e = 0; e < E; ++e) {
+        memset(skip, 0, (size_t)HW);
+        const uint32_t env_id = (uint32_t)(p->env_offset + e), step = rng_step ? rng_step[e] : 0u;
+        const uint32_t* tab = s_cdf + (long)wind_index[e] * 8 * PINEC_CDF;
+        int skipped_sources = 0;
+        for (long lin = 0; lin < HW; ++lin) {
+            if (grid_in[e * HW + lin] != p->fire) continue;
+            if (skip[lin]) {
+                ++skipped_sources;
+                continue;
+            }
+            const int r = (int)(lin / W), c = (int)(lin % W);
+            uint32_t b0[4];
+            const uint32_t c0[4] = {(uint32_t)lin, env_id, step, TAG_PINEC};
+            philox(c0, k0, k1, b0);
+            const int n = cdf_pick(b0[0], p->n_cdf, PINEC_NMAX);
+            for (int m = 0; m < n; ++m) {
+                uint32_t x[4];
+                const uint32_t cm[4] = {(uint32_t)lin, env_id, step, TAG_PINEC + 1u + (uint32_t)m};
+                philox(cm, k0, k1, x);
+                const int d = (int)(x[2] >> 29);
+                const uint32_t* t = tab + d * PINEC_CDF;
+                const int s = cdf_pick(x[0], t + 1, (int)t[0]) - (int)(t[0] >> 1);
+                const int tr = r + p->dx[d] * s, tc = c + p->dy[d] * s;
+                if (tr < 0 || tr >= H || tc < 0 || tc >= W || (tr == r && tc == c)) continue;
+                const long tl = (long)tr * W + tc;
+                int vv = veg[e * HW + tl], dd = den[e * HW + tl];
+                vv = vv < 1 ? 1 : (vv > 5 ? 5 : vv);
+                dd = dd < 1 ? 1 : (dd > 5 ? 5 : dd);
+                if (!((x[1] >> 8) < p->burn_thr[vv][dd])) continue;
+                const uint8_t prev = grid_out[e * HW + tl];
+                grid_out[e * HW + tl] = (uint8_t)p->fire;
+                uint32_t a[4];
+                const uint32_t ca[4] = {(uint32_t)tl, env_id, step, TAG_PINEC_AGE};
+                philox(ca, k0, k1, a);
+                age_out[e * HW + tl] = (int16_t)randint_ms(a[0], p->age_lo, p->age_hi);
+                if (counts && prev != p->fire) {
+                    if (prev == p->empty) counts[3 * e] -= 1;
+                    else if (prev == p->tree) counts[3 * e + 1] -= 1;
+                    counts[3 * e + 2] += 1;
+                }
+                if (tl > lin) skip[tl] = 1;
+            }
+        }
+        if (n_skipped_sources) n_skipped_sources[e] = skipped_sources;
+    }
+    free(skip);
+}

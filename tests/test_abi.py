@@ -68,6 +68,9 @@ int main(void) {
   printf("gca_pine_params %zu\n", sizeof(gca_pine_params));
   P(gca_pine_params, max_pinecones) P(gca_pine_params, dy) P(gca_pine_params, scale) P(gca_pine_params, den1p)
   P(gca_pine_params, seed) P(gca_pine_params, fire)
+  printf("gca_pine_classic_params %zu\n", sizeof(gca_pine_classic_params));
+  P(gca_pine_classic_params, dx) P(gca_pine_classic_params, burn_thr) P(gca_pine_classic_params, age_hi)
+  P(gca_pine_classic_params, seed) P(gca_pine_classic_params, fire)
   return 0;
 }
 """
@@ -84,7 +87,7 @@ def test_struct_layouts_match_the_header(tmp_path):
     got = dict(line.rsplit(" ", 1) for line in out if line)
     py = {"gca_bulldozer_params": _lib.BulldozerParams, "gca_alex_params": _lib.AlexParams,
           "gca_advenv_params": _lib.AdvEnvParams, "gca_obs_params": _lib.ObsParams,
-          "gca_pine_params": _lib.PineParams}
+          "gca_pine_params": _lib.PineParams, "gca_pine_classic_params": _lib.PineClassicParams}
     for key, val in got.items():
         if "." in key:
             t, f = key.split(".")

@@ -265,7 +265,7 @@ def test_classic_dropin_matches_classic_restatement(device, H, W, seed):
     ctx = cl.random_context(rng, H, W)
     dr = cl.random_draws(rng, H, W)
     ng, na, nw, rp = cl.update(ctx["grid"], ctx, dr, 0, 1, 2)
-    op = PartiallyObservableForestFire(0, 1, 2)
+    op = PartiallyObservableForestFire(0, 1, 2, pinecones=False)
     age_obj = ctx["fire_age"]
     new_grid, out_ctx, probs = op(ctx["grid"], None, ctx, draws=dr, return_probs=True)
     assert out_ctx is ctx and ctx["fire_age"] is age_obj  # context mutated in place
@@ -312,8 +312,9 @@ def test_classic_philox_bit_exact_vs_c_oracle(device, H, W):
         go, ao, co, _ = alex_c.alex_step(p, grid, age, veg, den, dous, ps, widx, rng_step=rs)
         g2, a2 = torch.empty_like(g_d), torch.empty_like(a_d)
         counts = torch.empty((E, 3), dtype=torch.int32, device=device)
+        rs_d = T(rs.view(np.int32), torch.int32)
         call("gca_alex_step", p, E, H, W, dev.ptr(g_d), dev.ptr(g2), dev.ptr(a_d), dev.ptr(a2), dev.ptr(v_d),
-             dev.ptr(n_d), dev.ptr(du_d), dev.ptr(ps_d), dev.ptr(w_d), dev.ptr(T(rs.view(np.int32), torch.int32)),
+             dev.ptr(n_d), dev.ptr(du_d), dev.ptr(ps_d), dev.ptr(w_d), dev.ptr(rs_d),
              None, None, None, None, dev.ptr(counts), st)
         assert np.array_equal(g2.cpu().numpy(), go) and np.array_equal(a2.cpu().numpy(), ao), f"step {step}"
         assert np.array_equal(counts.cpu().numpy(), co)
