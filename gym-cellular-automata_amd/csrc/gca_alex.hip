@@ -145,6 +145,22 @@ template <class T, class S> __device__ __forceinline__ T bitcast_(S s) {
 #ifndef GCA_ALEX_WGS
 #define GCA_ALEX_WGS 4
 #endif
+// GLDS (PK only): after the heat phase the column-prefix LDS is dead, so two of the seven edge-slope loads of the
+// direction pass (L2, L3, then L6) land there by LDS-DMA (global_load_lds_dwordx4, no VGPR destination) beside the
+// two-deep register ring (L0/L4, L1/L5): four loads in flight per wave instead of two. The ring and DMA loads are
+// inline asm, counted by hand (s_waitcnt vmcnt(N) with N = the loads issued after the one waited for); hipcc's own
+// loads are all retired before the first of them (the ties at the end of the heat phase). Bit-exact (the packed-kernel
+// GPU tests), but 2 % SLOWER on the headline (r02h: 1.460 vs 1.433 ms; profiles/r02h), so it stays off: more slope
+// bytes in flight is not what bounds the step.
+#ifndef GCA_ALEX_GLDS
+#define GCA_ALEX_GLDS 0
+#endif
+typedef float f4v __attribute__((ext_vector_type(4)));
+// bytes of the column-prefix region: (RR + 1) rows of CWP dwords; with GLDS at least the 4 waves x 8 KiB of slope slots
+// it hosts after the heat phase (small radii stage fewer rows)
+__host__ __device__ constexpr int cp_bytes(int RR, bool pk) {
+    return (GCA_ALEX_GLDS && pk && 4 * (RR + 1) * CWP < 32768) ? 32768 : 4 * (RR + 1) * CWP;
+}
 template <int R, int MODE, bool FAST, bool ES, bool PK = false>
 __global__ __launch_bounds__(256, GCA_ALEX_WGS) void alex_step_kernel(
     gca_alex_params p, int H, int W, int tiles_r, int tiles_c, const uint8_t* __restrict__ grid_in,
@@ -161,8 +177,9 @@ __global__ __launch_bounds__(256, GCA_ALEX_WGS) void alex_step_kernel(
     constexpr int NCH = CW / 16;       // 16-column chunks per staged row
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint32_t* CP = reinterpret_cast<uint32_t*>(smem);                                        // [RR+1][CWP]
-    uint16_t* FB = reinterpret_cast<uint16_t*>(smem + sizeof(uint32_t) * (RR + 1) * CWP);   // [RR][NCH] fire bits
-    float* LUT = reinterpret_cast<float*>(smem + sizeof(uint32_t) * (RR + 1) * CWP + sizeof(uint16_t) * RR * NCH);
+    constexpr int CPB = cp_bytes(RR, PK);                                                    // CP (+ GLDS slots)
+    uint16_t* FB = reinterpret_cast<uint16_t*>(smem + CPB);                                  // [RR][NCH] fire bits
+    float* LUT = reinterpret_cast<float*>(smem + CPB + sizeof(uint16_t) * RR * NCH);
     // LUT[0..7] = 1 + p_veg[clip(v, 1, 5)] for v = min(byte, 7); LUT[8..15] the same for density
 
     // XCD-aware order: blocks b, b+8, b+16, ... share an XCD (and its L2) under round-robin
@@ -258,9 +275,15 @@ __global__ __launch_bounds__(256, GCA_ALEX_WGS) void alex_step_kernel(
     constexpr int NPL = ES ? 4 : 8;
     const float* psE = p_slope + (size_t)e * NPL * HW;  // wave-uniform
     auto load_ps = [&](int k, float4 (&v)[4]) {
+#ifdef GCA_ABL_R1ROW  // ablation (wrong results): loads 4..6 re-read load 3's addresses instead of row r+1 (r02h: the
+                      // launch's FETCH then equals the algorithmic reads, 20.13 B/cell vs 24.05, at -1 % time)
+        const int plane = ES ? (k < 4 ? k : 3) : k;
+        const int dr = 0;
+#else
         const int plane = ES ? (k < 4 ? k : 6 - k) : k;
         // ES rows r+1 (k >= 4): row H-1 (a border row: every value killed) reads itself instead
         const int dr = (ES && k >= 4 && r + 1 < H) ? 1 : 0;
+#endif
         const float* src = psE + (uint32_t)(plane * (uint32_t)HW) + lo + (uint32_t)(dr * W);
         if (vec) {
             // PK: coalesced segment order, lane q's columns 16q + 4m .. +3 at segment position 64m + 4q
@@ -277,6 +300,46 @@ __global__ __launch_bounds__(256, GCA_ALEX_WGS) void alex_step_kernel(
         }
     };
     float4 psbuf[2][4];
+    // ---- GLDS: hand-counted slope loads (see GCA_ALEX_GLDS). Lane byte offset of load k in the env's planes
+    //      (PK segment order: lane q's float4 m at 64m - 12q floats from its cell offset) + offset:256m.
+    constexpr bool GL = PK && (GCA_ALEX_GLDS != 0);
+    f4v ring[2][4];
+    auto ps_off = [&](int k) -> uint32_t {
+        const int plane = k < 4 ? k : 6 - k;
+        const int dr = (k >= 4 && r + 1 < H) ? 1 : 0;
+        return 4u * ((uint32_t)plane * (uint32_t)HW + lo + (uint32_t)(dr * W)) - 48u * (uint32_t)q;
+    };
+    auto gl_ring = [&](int k, f4v (&v)[4]) {
+        const uint32_t o = ps_off(k);
+        asm volatile(
+            "global_load_dwordx4 %0, %4, %5\n\tglobal_load_dwordx4 %1, %4, %5 offset:256\n\t"
+            "global_load_dwordx4 %2, %4, %5 offset:512\n\tglobal_load_dwordx4 %3, %4, %5 offset:768"
+            : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3])
+            : "v"(o), "s"(psE)
+            : "memory");
+    };
+    // LDS slots (byte offsets in smem): wave w owns [8 KiB w, 8 KiB w + 8 KiB) of the dead column prefix; 4 KiB per
+    // load, instruction m's 1 KiB at +1024 m, lane l's 16 B at +16 l (the LDS-DMA's lane-linear image)
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t slot_off = 8192u * wv;
+    const uint32_t lds_base = (uint32_t)__builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)((__attribute__((address_space(3))) unsigned char*)smem) + slot_off);
+    auto gl_lds = [&](int k, uint32_t slot) {  // slot 0 / 1
+        const uint32_t o = ps_off(k);
+        const uint32_t b = lds_base + 4096u * slot;
+        uint32_t keep;
+        asm volatile(
+            "s_mov_b32 %0, m0\n\t"
+            "s_mov_b32 m0, %5\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %9\n\t"
+            "s_mov_b32 m0, %6\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %9\n\t"
+            "s_mov_b32 m0, %7\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %3, %9\n\t"
+            "s_mov_b32 m0, %8\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %4, %9\n\t"
+            "s_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "v"(o), "v"(o + 256u), "v"(o + 512u), "v"(o + 768u), "s"(b), "s"(b + 1024u), "s"(b + 2048u),
+              "s"(b + 3072u), "s"(psE)
+            : "memory");
+    };
     uint32_t agew[8];
     auto load_ages = [&]() {
         if (vec) {
@@ -580,9 +643,31 @@ __global__ __launch_bounds__(256, GCA_ALEX_WGS) void alex_step_kernel(
 #endif
 #pragma unroll
         for (int j = 0; j < 8; ++j) ph2[j] = ph2[j] - dz2[j];  // p_h = heat - dousing (:198)
+        if constexpr (!GL) {
 #if GCA_ALEX_WGS >= 4
-        load_ps(1, psbuf[1]);
+            load_ps(1, psbuf[1]);
 #endif
+        }
+    }
+    if constexpr (GL) {
+        // retire every hipcc-visible load now, on every path (L0, vegetation / density, the edge values; hipcc
+        // cannot tell that the two `wave_need` branches agree, so a tie inside the first one would leave them
+        // pending on its fall-through path and hipcc would drain the hand-counted loads at their first use): from
+        // here on the slope loads are hand-counted and no hipcc wait may drain them
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+            asm volatile("" : "+v"(psbuf[0][m].x), "+v"(psbuf[0][m].y), "+v"(psbuf[0][m].z), "+v"(psbuf[0][m].w));
+        asm volatile("" : "+v"(e4), "+v"(e5), "+v"(e7), "+v"(vgw[0]), "+v"(vgw[1]), "+v"(vgw[2]), "+v"(vgw[3]),
+                     "+v"(dnw[0]), "+v"(dnw[1]), "+v"(dnw[2]), "+v"(dnw[3]));
+        // every wave's heat-phase reads of the prefix are done (their values are in registers) before the DMA
+        // overwrites it; a raw barrier: __syncthreads()' fence would add nothing hipcc knows to wait for here
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (wave_need) {
+            gl_ring(1, ring[1]);
+            gl_lds(2, 0);
+            gl_lds(3, 1);
+        }
     }
 
     // ---- FIRE bits of rows r-1, r, r+1: bit j of nbw[a] <-> staged column cc0 - 1 + j (j = 0..17)
@@ -645,10 +730,44 @@ __global__ __launch_bounds__(256, GCA_ALEX_WGS) void alex_step_kernel(
                                                              : (f2){psc[j >> 1].x, psc[j >> 1].y};
             } else {
                 float a[16];
+                if constexpr (GL) {
+                    // hand-counted waits: N = slope loads issued after the one consumed (issue order L1 | L2 L3
+                    // (DMA) | L4 after d0 | L5 after d1 | L6 (DMA) after d2); L0 was retired by hipcc
+                    if (d == 1)
+                        asm volatile("s_waitcnt vmcnt(12)" : "+v"(ring[1][0]), "+v"(ring[1][1]), "+v"(ring[1][2]),
+                                     "+v"(ring[1][3])::"memory");
+                    if (d == 2 || d == 3) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+                    if (d == 5)
+                        asm volatile("s_waitcnt vmcnt(8)" : "+v"(ring[0][0]), "+v"(ring[0][1]), "+v"(ring[0][2]),
+                                     "+v"(ring[0][3])::"memory");
+                    if (d == 6)
+                        asm volatile("s_waitcnt vmcnt(4)" : "+v"(ring[1][0]), "+v"(ring[1][1]), "+v"(ring[1][2]),
+                                     "+v"(ring[1][3])::"memory");
+                    if (d == 7) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    if (ld == 0) {
 #pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const float4 v = psc[i >> 2];
-                    a[i] = (i & 3) == 0 ? v.x : (i & 3) == 1 ? v.y : (i & 3) == 2 ? v.z : v.w;
+                        for (int i = 0; i < 16; ++i) {
+                            const float4 v = psbuf[0][i >> 2];
+                            a[i] = (i & 3) == 0 ? v.x : (i & 3) == 1 ? v.y : (i & 3) == 2 ? v.z : v.w;
+                        }
+                    } else if (ld == 1 || ld == 4 || ld == 5) {
+#pragma unroll
+                        for (int i = 0; i < 16; ++i) a[i] = ring[ld & 1][i >> 2][i & 3];
+                    } else {  // L2 / L6: slot 0, L3: slot 1
+                        const unsigned char* sl = smem + slot_off + 4096u * (ld == 3 ? 1u : 0u) + 16u * (uint32_t)(tid & 63);
+#pragma unroll
+                        for (int m = 0; m < 4; ++m) {
+                            const f4v v = *reinterpret_cast<const f4v*>(sl + 1024 * m);
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) a[4 * m + j] = v[j];
+                        }
+                    }
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        const float4 v = psc[i >> 2];
+                        a[i] = (i & 3) == 0 ? v.x : (i & 3) == 1 ? v.y : (i & 3) == 2 ? v.z : v.w;
+                    }
                 }
                 // d = 4, 7: element i <- i + 1 (cell i's right / down-right neighbour);
                 // d = 5: element i <- i - 1; the row segment's outer element comes from the next /
@@ -719,7 +838,16 @@ __global__ __launch_bounds__(256, GCA_ALEX_WGS) void alex_step_kernel(
             for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(qn2[j]));  // finish this direction's products here
             // refill the buffer just consumed with load ld + 2 (ES: not after d = 3, whose load d = 4 reuses)
             const int last = ES ? 6 : 7;
-            if (ld + 2 <= last && !(ES && d == 3)) load_ps(ld + 2, psc);
+            if constexpr (GL) {
+                if (d == 0) gl_ring(4, ring[0]);
+                if (d == 1) gl_ring(5, ring[1]);
+                if (d == 2) {  // slot 0 read (its values are in registers) before the DMA refills it
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    gl_lds(6, 0);
+                }
+            } else if (ld + 2 <= last && !(ES && d == 3)) {
+                load_ps(ld + 2, psc);
+            }
             if (d == 6) load_ages();            // its buffer is free from here on
             __builtin_amdgcn_sched_barrier(0);  // two loads' 64 B per lane in flight
         }
@@ -886,7 +1014,7 @@ void launch_alex(const gca_alex_params& p, int E, int H, int W, const uint8_t* g
     const int tiles_r = (H + TH - 1) / TH, tiles_c = (W + TW - 1) / TW;
     constexpr int RS = R < 2 ? 2 : R;
     constexpr int RR = TH + 2 * RS;
-    const size_t lds = sizeof(uint32_t) * (RR + 1) * CWP + sizeof(uint16_t) * RR * (CW / 16) + sizeof(float) * 16;
+    const size_t lds = (size_t)cp_bytes(RR, PK) + sizeof(uint16_t) * RR * (CW / 16) + sizeof(float) * 16;
     const dim3 grid((unsigned)((int64_t)E * tiles_r * tiles_c));
     const bool fast = MODE == 0 && W % TW == 0 && H % TH == 0 &&
                       ((((uintptr_t)gi) | ((uintptr_t)go) | ((uintptr_t)ai) | ((uintptr_t)ao) | ((uintptr_t)veg) |
@@ -910,8 +1038,12 @@ void dispatch_r(int R, const gca_alex_params& p, int E, int H, int W, const uint
 #define GCA_ALEX_CASE(RV) \
     case RV: launch_alex<RV, MODE, ES, PK>(p, E, H, W, gi, go, ai, ao, veg, den, dous, ps, wi, rs, ib, ig, ia, po, counts, st, act_in, act_out); break;
     switch (R) {
+#ifdef GCA_ALEX_ONLY_R  // ISA inspection builds: one radius only
+        GCA_ALEX_CASE(GCA_ALEX_ONLY_R)
+#else
         GCA_ALEX_CASE(1) GCA_ALEX_CASE(2) GCA_ALEX_CASE(3) GCA_ALEX_CASE(4)
         GCA_ALEX_CASE(5) GCA_ALEX_CASE(6) GCA_ALEX_CASE(7) GCA_ALEX_CASE(8)
+#endif
     }
 #undef GCA_ALEX_CASE
 }
