@@ -39,6 +39,9 @@
 #ifndef GCA_OBS_BATCH
 #define GCA_OBS_BATCH 1  // full rounds: 3 LDS reads, one wait, 3 stores (A/B hook)
 #endif
+#ifndef GCA_OBS_NB
+#define GCA_OBS_NB 1  // blocks per workgroup (A/B hook): > 1 chains blocks of one env with the next one's staging prefetched
+#endif
 #ifndef GCA_OBS_NT
 #define GCA_OBS_NT 1  // non-temporal RGB stores (r01i A/B: 1.07 vs 1.10 ms per 4096 x 256^2)
 #endif
@@ -114,7 +117,7 @@ __device__ __forceinline__ void render(const gca_obs_params& p, float* __restric
 // block's rows plus one halo row on each side are staged in LDS for the blur; W % 4 == 0 renders
 // 4 cells per thread (3 float4 stores, 48-B aligned).
 __global__ __launch_bounds__(256) void adv_observation_kernel(gca_obs_params p, int mode, int H, int W, int RB,
-                                                              int blocks_per_env, const uint8_t* __restrict__ grid,
+                                                              int blocks_per_env, int nbw, const uint8_t* __restrict__ grid,
                                                               const uint8_t* __restrict__ dousing,
                                                               const int32_t* __restrict__ pos,
                                                               const int32_t* __restrict__ is_night,
@@ -124,10 +127,13 @@ __global__ __launch_bounds__(256) void adv_observation_kernel(gca_obs_params p, 
                                                               const uint8_t* __restrict__ env_mask) {
     extern __shared__ uint8_t T[];  // [(RB + 2) * W] grid rows r0-1 .. r0+RB (edge-clamped), then [RB * W] dousing
     uint8_t* D = T + (RB + 2) * W;
-    const int e = blockIdx.x / blocks_per_env;
+    // nbw > 1: this workgroup renders blocks nbw*b .. nbw*b + nbw-1, all of one env (blocks_per_env % nbw == 0, checked
+    // on the host), the next block's staging loads in flight while the current one renders
+    const int blk0 = (int)blockIdx.x * nbw;
+    const int e = blk0 / blocks_per_env;
     if (env_mask && !env_mask[e]) return;  // whole block: envs outside the mask keep their observation
-    const int r0 = (blockIdx.x - e * blocks_per_env) * RB;
-    const int rows = min(RB, H - r0);
+    int r0 = (blk0 - e * blocks_per_env) * RB;
+    int rows = min(RB, H - r0);
     const int64_t HW = (int64_t)H * W;
     const uint8_t* g = grid + e * HW;
     const uint8_t* du = dousing ? dousing + e * HW : nullptr;
@@ -153,22 +159,26 @@ __global__ __launch_bounds__(256) void adv_observation_kernel(gca_obs_params p, 
     const bool al16 = ((((uintptr_t)grid) | ((uintptr_t)dousing)) & 15u) == 0;
     const bool fast16 = do_stage && (W & 15) == 0 && al16;
     const int w16 = W >> 4;
-    const int ng16 = (rows + 2) * w16, nd16 = du ? rows * w16 : 0;
-    const int nst = fast16 ? ng16 + nd16 : 0;
+    int ng16 = (rows + 2) * w16, nd16 = du ? rows * w16 : 0;
+    int nst = fast16 ? ng16 + nd16 : 0;
     // byte offset of staged 16-B chunk idx (grid rows r0-1 .. r0+rows edge-clamped, then the dousing rows)
     // from g; the dousing array is addressed relative to the grid (same env, same layout)
     const int64_t dgap = du ? (int64_t)(du - g) : 0;
-    auto src16 = [&](int idx) -> int64_t {
+    auto src16b = [&](int idx, int b0, int bng) -> int64_t {  // chunk idx of the block starting at row b0
         const int lr = idx / w16, cq = idx - lr * w16;
-        const int r = min(max(r0 - 1 + lr, 0), H - 1);
-        return idx < ng16 ? (int64_t)r * W + 16 * cq : dgap + (int64_t)r0 * W + 16 * (int64_t)(idx - ng16);
+        const int r = min(max(b0 - 1 + lr, 0), H - 1);
+        return idx < bng ? (int64_t)r * W + 16 * cq : dgap + (int64_t)b0 * W + 16 * (int64_t)(idx - bng);
     };
+    auto src16 = [&](int idx) -> int64_t { return src16b(idx, r0, ng16); };
     uint4 pre[GCA_OBS_PRE];
+    auto issue_pre = [&](int b0, int bng, int bnst) {  // unconditional loads of clamped chunks: pre stays in VGPRs
 #pragma unroll
-    for (int j = 0; j < GCA_OBS_PRE; ++j) {  // unconditional loads of clamped chunks: pre stays in VGPRs
-        const int idx = min((int)threadIdx.x + 256 * j, max(nst - 1, 0));
-        pre[j] = nst ? *reinterpret_cast<const uint4*>(g + src16(idx)) : make_uint4(0u, 0u, 0u, 0u);
-    }
+        for (int j = 0; j < GCA_OBS_PRE; ++j) {
+            const int idx = min((int)threadIdx.x + 256 * j, max(bnst - 1, 0));
+            pre[j] = bnst ? *reinterpret_cast<const uint4*>(g + src16b(idx, b0, bng)) : make_uint4(0u, 0u, 0u, 0u);
+        }
+    };
+    issue_pre(r0, ng16, nst);
 
     // ---- display selection (see the header comment in include/gca.h). Every wave scans on its own (the
     //      result is a function of the grid alone, so all waves agree): no workgroup barrier per scanned row
@@ -232,6 +242,15 @@ __global__ __launch_bounds__(256) void adv_observation_kernel(gca_obs_params p, 
         render_kind(p, c3, (int)threadIdx.x / 3, (int)threadIdx.x % 3, k.night);
         COLT[threadIdx.x] = make_float4(c3[0], c3[1], c3[2], 0.0f);
     }
+    for (int bi = 0; bi < nbw; ++bi) {
+    if (bi > 0) {  // the next block of the same env: every wave is done reading the previous block's LDS rows
+        r0 += RB;
+        rows = min(RB, H - r0);
+        ng16 = (rows + 2) * w16;
+        nd16 = du ? rows * w16 : 0;
+        nst = fast16 ? ng16 + nd16 : 0;
+        __syncthreads();
+    }
     if (do_stage) {
         if (fast16) {
 #pragma unroll
@@ -242,6 +261,11 @@ __global__ __launch_bounds__(256) void adv_observation_kernel(gca_obs_params p, 
             for (int idx = (int)threadIdx.x + 256 * GCA_OBS_PRE; idx < ng16 + nd16; idx += 256)
                 reinterpret_cast<uint4*>(idx < ng16 ? T : D - 16 * ng16)[idx] =
                     *reinterpret_cast<const uint4*>(g + src16(idx));
+            if (bi + 1 < nbw) {  // the next block's staging loads fly while this one renders
+                const int nb0 = r0 + RB, nrows = min(RB, H - nb0);
+                const int nng = (nrows + 2) * w16;
+                issue_pre(nb0, nng, nng + (du ? nrows * w16 : 0));
+            }
         } else if (stage_all) {
             const int wq = W >> 2;
             const int ng = (rows + 2) * wq, nd = du ? rows * wq : 0;
@@ -393,6 +417,7 @@ __global__ __launch_bounds__(256) void adv_observation_kernel(gca_obs_params p, 
             }
         }
     }
+    }  // blocks of this workgroup
 }
 
 }  // namespace
@@ -412,8 +437,10 @@ extern "C" int gca_adv_observation(const gca_obs_params* p, int mode, int E, int
     // rows per block; (2 RB + 2) * W bytes of dynamic LDS (grid + dousing), at most 48 KiB
     const int RB = max(1, min(GCA_OBS_RB, 24576 / W - 1));
     const int bpe = (H + RB - 1) / RB;
-    hipLaunchKernelGGL(adv_observation_kernel, dim3((unsigned)((int64_t)E * bpe)), dim3(256), (size_t)(2 * RB + 2) * W,
-                       (hipStream_t)stream, *p, mode, H, W, RB, bpe, grid, dousing, pos, is_night, time_step, action,
+    // blocks per workgroup: the production shape (step mode, W % 16 == 0) chains GCA_OBS_NB blocks of one env
+    const int nbw = (mode == 0 && W % 16 == 0 && bpe % GCA_OBS_NB == 0) ? GCA_OBS_NB : 1;
+    hipLaunchKernelGGL(adv_observation_kernel, dim3((unsigned)((int64_t)E * bpe / nbw)), dim3(256), (size_t)(2 * RB + 2) * W,
+                       (hipStream_t)stream, *p, mode, H, W, RB, bpe, nbw, grid, dousing, pos, is_night, time_step, action,
                        action_stride, rgb, channels, env_mask);
     GCA_CHECK_LAUNCH("adv_observation");
     return GCA_OK;

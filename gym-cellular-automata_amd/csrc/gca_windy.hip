@@ -243,6 +243,168 @@ __global__ __launch_bounds__(256) void windy_fast_kernel(uint8_t* __restrict__ b
     }
 }
 
+// ------------------------------------------------------------------ row-stream kernel (W = 256 NW, NW = 1, 2)
+// The fast kernel's rule with a different lane map: a wave holds WHOLE image rows, lane l owning columns
+// [4 NW l, 4 NW l + 4 NW) (one dword per row at W = 256), and marches down a strip of SH rows. The vertical
+// neighbours are then the lane's own previous / next row (registers: no cross-lane traffic at all) and the horizontal
+// ones the neighbour lanes' edge dwords, moved by DPP whole-wave shifts (wave_shr:1 / wave_shl:1, lanes 0 / 63 read 0 =
+// the grid's left / right border) instead of ds_bpermute. Each row's fire flags and their two column shifts are built
+// once and used by the three output rows that see them. Loads run GCA_WINDY_RD rows ahead (one dword per lane each, so
+// many rows fit in flight); row indices are clamped, not branched, so hipcc keeps the counted waits.
+#ifndef GCA_WINDY_ROWS
+#define GCA_WINDY_ROWS 1  // 0: the 16-cells-per-lane fast kernel for every W
+#endif
+#ifndef GCA_WINDY_RSH
+#define GCA_WINDY_RSH 32  // strip height per wave
+#endif
+#ifndef GCA_WINDY_RD
+#define GCA_WINDY_RD 8  // rows in flight ahead of the row being classified
+#endif
+
+template <int NW>
+struct RowRaw {
+    uint32_t w[NW];
+};
+template <int NW>
+struct RowCls {
+    uint32_t f[NW], fl[NW], fr[NW];  // FIRE flags (0x01 per byte); byte i = flag of column c-1 (fl), c+1 (fr)
+    uint32_t t[NW];                  // TREE flags
+};
+
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t v) {  // lane l <- lane l-1, lane 0 <- 0
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, true);
+}
+__device__ __forceinline__ uint32_t wave_shl1(uint32_t v) {  // lane l <- lane l+1, lane 63 <- 0
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, true);
+}
+
+template <int NW>
+__device__ __forceinline__ RowRaw<NW> load_rowraw(const uint8_t* __restrict__ S, int R, int H) {
+    constexpr int W = 256 * NW;
+    const int Rc = min(max(R, 0), H - 1);  // clamped: the value of an out-of-grid row is discarded by classify
+    const uint8_t* p = S + (int64_t)Rc * W;
+    RowRaw<NW> x;
+    if (NW == 1) {
+        x.w[0] = *reinterpret_cast<const uint32_t*>(p);
+    } else if (NW == 2) {
+        const uint2 v = *reinterpret_cast<const uint2*>(p);
+        x.w[0] = v.x; x.w[1 % NW] = v.y;
+    } else {
+        const uint4 v = *reinterpret_cast<const uint4*>(p);
+        x.w[0] = v.x; x.w[1 % NW] = v.y; x.w[2 % NW] = v.z; x.w[3 % NW] = v.w;
+    }
+    return x;
+}
+
+template <int NW>
+__device__ __forceinline__ RowCls<NW> classify_row(const RowRaw<NW>& x, bool valid, uint32_t Tp, uint32_t Fp) {
+    RowCls<NW> o;
+#pragma unroll
+    for (int j = 0; j < NW; ++j) {
+        o.f[j] = valid ? bytes_eq01(x.w[j], Fp) : 0u;
+        o.t[j] = valid ? bytes_eq01(x.w[j], Tp) : 0u;
+    }
+    const uint32_t prev = wave_shr1(o.f[NW - 1]), next = wave_shl1(o.f[0]);
+#pragma unroll
+    for (int j = 0; j < NW; ++j) {
+        o.fl[j] = __builtin_amdgcn_alignbyte(o.f[j], j ? o.f[j - 1] : prev, 3);
+        o.fr[j] = __builtin_amdgcn_alignbyte(j < NW - 1 ? o.f[j + 1] : next, o.f[j], 1);
+    }
+    return o;
+}
+
+template <int NW>
+__global__ __launch_bounds__(256) void windy_rows_kernel(uint8_t* __restrict__ buf0, uint8_t* __restrict__ buf1,
+                                                         const uint8_t* __restrict__ parity,
+                                                         const int32_t* __restrict__ steps, int pass,
+                                                         const uint8_t* __restrict__ dir_mask, int H,
+                                                         int blocks_per_env, uint32_t Ep, uint32_t Tp, uint32_t Fp,
+                                                         int32_t* __restrict__ counts) {
+    constexpr int W = 256 * NW;
+    constexpr int SH = GCA_WINDY_RSH;
+    constexpr int RD = GCA_WINDY_RD;
+    const int env = blockIdx.x / blocks_per_env;
+    const int sblk = blockIdx.x - env * blocks_per_env;
+    if (steps && steps[env] <= pass) return;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int s0 = (sblk * 4 + wave) * SH;
+    if (s0 >= H) return;
+    const bool odd = parity && parity[env];
+    const int64_t HW = (int64_t)H * W;
+    const uint8_t* __restrict__ S = (odd ? buf1 : buf0) + (int64_t)env * HW + 4 * NW * lane;
+    uint8_t* __restrict__ Dst = (odd ? buf0 : buf1) + (int64_t)env * HW + 4 * NW * lane;
+    const uint32_t m = dir_mask[env];
+    const uint32_t m0 = (m & 1u) ? ~0u : 0u, m1 = (m & 2u) ? ~0u : 0u, m2 = (m & 4u) ? ~0u : 0u,
+                   m3 = (m & 8u) ? ~0u : 0u, m4 = (m & 16u) ? ~0u : 0u, m5 = (m & 32u) ? ~0u : 0u,
+                   m6 = (m & 64u) ? ~0u : 0u, m7 = (m & 128u) ? ~0u : 0u;
+
+    // ring[k % RD] holds row s0 + 1 + k (k = 0 .. SH): the strip's rows below row s0 up to its lower halo row
+    RowRaw<NW> ring[RD];
+    const RowRaw<NW> r_up = load_rowraw<NW>(S, s0 - 1, H), r_cur = load_rowraw<NW>(S, s0, H);
+#pragma unroll
+    for (int k = 0; k < RD; ++k) ring[k] = load_rowraw<NW>(S, s0 + 1 + k, H);
+    RowCls<NW> A = classify_row<NW>(r_up, s0 >= 1, Tp, Fp);
+    RowCls<NW> B = classify_row<NW>(r_cur, true, Tp, Fp);
+
+    int32_t cntT = 0, cntF = 0, cntV = 0;
+#pragma unroll
+    for (int t = 0; t < SH; ++t) {
+        const int Rc = s0 + t;
+        // row Rc + 1: loaded RD rows ago; its slot is refilled with row Rc + 1 + RD right away
+        const RowCls<NW> C = classify_row<NW>(ring[t % RD], Rc + 1 < H, Tp, Fp);
+        if (t + RD < SH) ring[t % RD] = load_rowraw<NW>(S, Rc + 1 + RD, H);
+        uint32_t outw[NW];
+        int32_t rowT = 0, rowF = 0;
+#pragma unroll
+        for (int j = 0; j < NW; ++j) {
+            // d -> source (r+1-a, c+1-b): d0 down/c+1, d1 down, d2 down/c-1, d3 cur/c+1, d4 cur/c-1, d5 up/c+1,
+            // d6 up, d7 up/c-1 (as windy_fast_kernel)
+            const uint32_t any = (C.fr[j] & m0) | (C.f[j] & m1) | (C.fl[j] & m2) | (B.fr[j] & m3) | (B.fl[j] & m4) |
+                                 (A.fr[j] & m5) | (A.f[j] & m6) | (A.fl[j] & m7);
+            const uint32_t ign = B.t[j] & any;    // TREE -> FIRE
+            const uint32_t keep = B.t[j] & ~any;  // TREE stays
+            const uint32_t ignm = (ign << 8) - ign, keepm = (keep << 8) - keep;
+            outw[j] = (ignm & Fp) | (keepm & Tp) | (~(ignm | keepm) & Ep);
+            rowF += __popc(ign);
+            rowT += __popc(keep);
+        }
+        if (Rc < H && t < SH) {
+            uint8_t* p = Dst + (int64_t)Rc * W;
+            if (NW == 1) *reinterpret_cast<uint32_t*>(p) = outw[0];
+            else if (NW == 2) *reinterpret_cast<uint2*>(p) = make_uint2(outw[0], outw[1 % NW]);
+            else *reinterpret_cast<uint4*>(p) = make_uint4(outw[0], outw[1 % NW], outw[2 % NW], outw[3 % NW]);
+            cntV += 4 * NW;
+            cntT += rowT;
+            cntF += rowF;
+        }
+        A = B;
+        B = C;
+    }
+    if (counts) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            cntT += __shfl_xor(cntT, off);
+            cntF += __shfl_xor(cntF, off);
+            cntV += __shfl_xor(cntV, off);
+        }
+        if (lane == 0) {
+            atomicAdd(counts + 3 * env + 0, cntV - cntT - cntF);
+            atomicAdd(counts + 3 * env + 1, cntT);
+            atomicAdd(counts + 3 * env + 2, cntF);
+        }
+    }
+}
+
+template <int NW>
+static void launch_rows(uint8_t* b0, uint8_t* b1, const uint8_t* parity, const int32_t* steps, int pass,
+                        const uint8_t* dm, int E, int H, int empty, int tree, int fire, int32_t* counts,
+                        hipStream_t st) {
+    const int strips = (H + GCA_WINDY_RSH - 1) / GCA_WINDY_RSH;
+    const int bpe = (strips + 3) / 4;
+    hipLaunchKernelGGL(windy_rows_kernel<NW>, dim3((unsigned)((int64_t)E * bpe)), dim3(256), 0, st, b0, b1, parity,
+                       steps, pass, dm, H, bpe, rep4(empty), rep4(tree), rep4(fire), counts);
+}
+
 // ------------------------------------------------------------------ host API
 extern "C" int gca_windy_dirmask(const double* wind, int64_t wind_stride, const double* roll, uint64_t seed,
                                  const uint32_t* rng_step, const int32_t* steps, int pass, int env_offset,
@@ -289,7 +451,11 @@ extern "C" int gca_windy_step(uint8_t* buf0, uint8_t* buf1, const uint8_t* parit
     const bool aligned = ((((uintptr_t)buf0) | ((uintptr_t)buf1)) & 15u) == 0;
     const int LPR = W / 16;
     const bool fast = !force_exact && empty == 0 && aligned && (W % 16 == 0) && LPR >= 1 && LPR <= 64 && (64 % LPR) == 0;
-    if (fast) {
+    if (fast && GCA_WINDY_ROWS && (W == 256 || W == 512)) {
+        if (W == 256) launch_rows<1>(buf0, buf1, parity, steps, pass, dir_mask, E, H, empty, tree, fire, counts, st);
+        else launch_rows<2>(buf0, buf1, parity, steps, pass, dir_mask, E, H, empty, tree, fire, counts, st);
+        GCA_CHECK_LAUNCH("windy_rows");
+    } else if (fast) {
         switch (LPR) {
             case 1: launch_fast<1>(buf0, buf1, parity, steps, pass, dir_mask, E, H, empty, tree, fire, counts, st); break;
             case 2: launch_fast<2>(buf0, buf1, parity, steps, pass, dir_mask, E, H, empty, tree, fire, counts, st); break;
