@@ -215,7 +215,8 @@ def bench_alex(args, world, rank, device, pg):
     E, N = args.envs, args.size
     env = AdvancedForestFireBulldozerEnv(N, N, key=1, num_envs=E, use_hidden=False, device=device,
                                          env_offset=rank * E, slope_layout=args.slope_layout, observation="rgb",
-                                         enable_extensions=True, tile_skip=args.tile_skip)
+                                         enable_extensions=os.environ.get("GCA_BENCH_EXT", "1") != "0",
+                                         tile_skip=args.tile_skip)
     env.reset()
     synthetic_state(env, rank, device)
     action = torch.zeros((E, 2), dtype=torch.int32, device=device)
@@ -270,10 +271,25 @@ def bench_alex(args, world, rank, device, pg):
             env.render_observation(action3)
 
     dt_rgb, kern_rgb = timed_loop(step_rgb, args.steps, args.warmup, pg, device, reps=3, prepare=prep)
+
+    def step_fill(events):  # the same loop with a write-only fill_ of the RGB buffer in place of the observation
+        step(None)
+        if events is not None:
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            env.rgb.fill_(0.5)
+            b.record()
+            events.append((a, b))
+        else:
+            env.rgb.fill_(0.5)
+
+    _, kern_fill = timed_loop(step_fill, args.steps, args.warmup, pg, device, reps=1, prepare=prep)
     res["with_rgb_observation"] = {"env_steps_per_s": world * E * args.steps / dt_rgb,
                                    "cell_updates_per_s": world * E * N * N * args.steps / dt_rgb,
                                    "obs_kernel_ms": kern_rgb * 1e3,
                                    "obs_gbs": 14 * E * N * N / kern_rgb / 1e9,
+                                   "same_buffer_fill_ms": kern_fill * 1e3,
+                                   "obs_frac_of_fill": kern_fill / kern_rgb,
                                    "note": "RGB f32 observation per step like the reference's stateless_step"}
     # the same env from its reset state (two burning cells per env, advanced_bulldozer.py:650-688): a
     # real episode's first steps, where the fire-sparsity skip leaves most waves the 7 B/cell of

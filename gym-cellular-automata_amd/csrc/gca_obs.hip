@@ -39,8 +39,9 @@
 #ifndef GCA_OBS_BATCH
 #define GCA_OBS_BATCH 1  // full rounds: 3 LDS reads, one wait, 3 stores (A/B hook)
 #endif
-#ifndef GCA_OBS_NB
-#define GCA_OBS_NB 1  // blocks per workgroup (A/B hook): > 1 chains blocks of one env with the next one's staging prefetched
+#ifndef GCA_OBS_PLAIN
+#define GCA_OBS_PLAIN 1  // chunks of 256 cells per wave in adv_obs_plain_kernel (0: always the staged kernel; r02k with
+                         // extensions off: 1 / 8 / 16 chunks -> 0.633 / 0.726 / 0.726 ms, staged kernel 0.688 ms)
 #endif
 #ifndef GCA_OBS_NT
 #define GCA_OBS_NT 1  // non-temporal RGB stores (r01i A/B: 1.07 vs 1.10 ms per 4096 x 256^2)
@@ -117,7 +118,7 @@ __device__ __forceinline__ void render(const gca_obs_params& p, float* __restric
 // block's rows plus one halo row on each side are staged in LDS for the blur; W % 4 == 0 renders
 // 4 cells per thread (3 float4 stores, 48-B aligned).
 __global__ __launch_bounds__(256) void adv_observation_kernel(gca_obs_params p, int mode, int H, int W, int RB,
-                                                              int blocks_per_env, int nbw, const uint8_t* __restrict__ grid,
+                                                              int blocks_per_env, const uint8_t* __restrict__ grid,
                                                               const uint8_t* __restrict__ dousing,
                                                               const int32_t* __restrict__ pos,
                                                               const int32_t* __restrict__ is_night,
@@ -127,13 +128,10 @@ __global__ __launch_bounds__(256) void adv_observation_kernel(gca_obs_params p, 
                                                               const uint8_t* __restrict__ env_mask) {
     extern __shared__ uint8_t T[];  // [(RB + 2) * W] grid rows r0-1 .. r0+RB (edge-clamped), then [RB * W] dousing
     uint8_t* D = T + (RB + 2) * W;
-    // nbw > 1: this workgroup renders blocks nbw*b .. nbw*b + nbw-1, all of one env (blocks_per_env % nbw == 0, checked
-    // on the host), the next block's staging loads in flight while the current one renders
-    const int blk0 = (int)blockIdx.x * nbw;
-    const int e = blk0 / blocks_per_env;
+    const int e = blockIdx.x / blocks_per_env;
     if (env_mask && !env_mask[e]) return;  // whole block: envs outside the mask keep their observation
-    int r0 = (blk0 - e * blocks_per_env) * RB;
-    int rows = min(RB, H - r0);
+    const int r0 = (blockIdx.x - e * blocks_per_env) * RB;
+    const int rows = min(RB, H - r0);
     const int64_t HW = (int64_t)H * W;
     const uint8_t* g = grid + e * HW;
     const uint8_t* du = dousing ? dousing + e * HW : nullptr;
@@ -159,26 +157,22 @@ __global__ __launch_bounds__(256) void adv_observation_kernel(gca_obs_params p, 
     const bool al16 = ((((uintptr_t)grid) | ((uintptr_t)dousing)) & 15u) == 0;
     const bool fast16 = do_stage && (W & 15) == 0 && al16;
     const int w16 = W >> 4;
-    int ng16 = (rows + 2) * w16, nd16 = du ? rows * w16 : 0;
-    int nst = fast16 ? ng16 + nd16 : 0;
+    const int ng16 = (rows + 2) * w16, nd16 = du ? rows * w16 : 0;
+    const int nst = fast16 ? ng16 + nd16 : 0;
     // byte offset of staged 16-B chunk idx (grid rows r0-1 .. r0+rows edge-clamped, then the dousing rows)
     // from g; the dousing array is addressed relative to the grid (same env, same layout)
     const int64_t dgap = du ? (int64_t)(du - g) : 0;
-    auto src16b = [&](int idx, int b0, int bng) -> int64_t {  // chunk idx of the block starting at row b0
+    auto src16 = [&](int idx) -> int64_t {
         const int lr = idx / w16, cq = idx - lr * w16;
-        const int r = min(max(b0 - 1 + lr, 0), H - 1);
-        return idx < bng ? (int64_t)r * W + 16 * cq : dgap + (int64_t)b0 * W + 16 * (int64_t)(idx - bng);
+        const int r = min(max(r0 - 1 + lr, 0), H - 1);
+        return idx < ng16 ? (int64_t)r * W + 16 * cq : dgap + (int64_t)r0 * W + 16 * (int64_t)(idx - ng16);
     };
-    auto src16 = [&](int idx) -> int64_t { return src16b(idx, r0, ng16); };
     uint4 pre[GCA_OBS_PRE];
-    auto issue_pre = [&](int b0, int bng, int bnst) {  // unconditional loads of clamped chunks: pre stays in VGPRs
 #pragma unroll
-        for (int j = 0; j < GCA_OBS_PRE; ++j) {
-            const int idx = min((int)threadIdx.x + 256 * j, max(bnst - 1, 0));
-            pre[j] = bnst ? *reinterpret_cast<const uint4*>(g + src16b(idx, b0, bng)) : make_uint4(0u, 0u, 0u, 0u);
-        }
-    };
-    issue_pre(r0, ng16, nst);
+    for (int j = 0; j < GCA_OBS_PRE; ++j) {  // unconditional loads of clamped chunks: pre stays in VGPRs
+        const int idx = min((int)threadIdx.x + 256 * j, max(nst - 1, 0));
+        pre[j] = nst ? *reinterpret_cast<const uint4*>(g + src16(idx)) : make_uint4(0u, 0u, 0u, 0u);
+    }
 
     // ---- display selection (see the header comment in include/gca.h). Every wave scans on its own (the
     //      result is a function of the grid alone, so all waves agree): no workgroup barrier per scanned row
@@ -242,15 +236,6 @@ __global__ __launch_bounds__(256) void adv_observation_kernel(gca_obs_params p, 
         render_kind(p, c3, (int)threadIdx.x / 3, (int)threadIdx.x % 3, k.night);
         COLT[threadIdx.x] = make_float4(c3[0], c3[1], c3[2], 0.0f);
     }
-    for (int bi = 0; bi < nbw; ++bi) {
-    if (bi > 0) {  // the next block of the same env: every wave is done reading the previous block's LDS rows
-        r0 += RB;
-        rows = min(RB, H - r0);
-        ng16 = (rows + 2) * w16;
-        nd16 = du ? rows * w16 : 0;
-        nst = fast16 ? ng16 + nd16 : 0;
-        __syncthreads();
-    }
     if (do_stage) {
         if (fast16) {
 #pragma unroll
@@ -261,11 +246,6 @@ __global__ __launch_bounds__(256) void adv_observation_kernel(gca_obs_params p, 
             for (int idx = (int)threadIdx.x + 256 * GCA_OBS_PRE; idx < ng16 + nd16; idx += 256)
                 reinterpret_cast<uint4*>(idx < ng16 ? T : D - 16 * ng16)[idx] =
                     *reinterpret_cast<const uint4*>(g + src16(idx));
-            if (bi + 1 < nbw) {  // the next block's staging loads fly while this one renders
-                const int nb0 = r0 + RB, nrows = min(RB, H - nb0);
-                const int nng = (nrows + 2) * w16;
-                issue_pre(nb0, nng, nng + (du ? nrows * w16 : 0));
-            }
         } else if (stage_all) {
             const int wq = W >> 2;
             const int ng = (rows + 2) * wq, nd = du ? rows * wq : 0;
@@ -417,7 +397,88 @@ __global__ __launch_bounds__(256) void adv_observation_kernel(gca_obs_params p, 
             }
         }
     }
-    }  // blocks of this workgroup
+}
+
+// Plain step observation (no extension channels, no grid transform — the env's default, enable_extensions = False):
+// every cell's colour depends on its own grid and dousing bytes (and the bulldozer's position) only, so there is no
+// halo and nothing to stage. Each wave renders CW chunks of 256 consecutive cells of one env (64 lanes x 4 cells: one
+// dword of grid and one of dousing per lane per chunk, all CW chunks' loads issued up front), looks the colours up in a
+// per-block LDS table (day and night x kind x dousing 0 / 1 / >= 2, built by the same `render_kind` arithmetic) and
+// writes each chunk's 3 KiB of RGB through its own LDS slice so that every non-temporal store instruction writes 1 KiB
+// contiguous. Straight-line code (CW is a template constant): hipcc's counted waits then let the stores of earlier
+// chunks stay in flight while later chunks render (a rolled loop made it wait for them: 0.65 ms per frame).
+// Requires (H*W / 256) % CW == 0 (a wave's chunks lie in one env; checked on the host).
+template <int CW>
+__global__ __launch_bounds__(256) void adv_obs_plain_kernel(gca_obs_params p, int64_t chunks, int chunks_per_env,
+                                                            int W, const uint8_t* __restrict__ grid,
+                                                            const uint8_t* __restrict__ dousing,
+                                                            const int32_t* __restrict__ pos,
+                                                            const int32_t* __restrict__ is_night,
+                                                            const int32_t* __restrict__ time_step,
+                                                            float* __restrict__ rgb, const uint8_t* __restrict__ env_mask) {
+    __shared__ float4 COL[2][12];
+    __shared__ float4 OUT4s[4][192];
+    if (threadIdx.x < 24) {
+        float c3[3];
+        const int nt = (int)threadIdx.x / 12, i = (int)threadIdx.x % 12;
+        render_kind(p, c3, i / 3, i % 3, nt != 0);
+        COL[nt][i] = make_float4(c3[0], c3[1], c3[2], 0.0f);
+    }
+    __syncthreads();
+    const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6), lane = (int)threadIdx.x & 63;
+    float4* OUT4 = OUT4s[wave];
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const int64_t c0 = ((int64_t)blockIdx.x * 4 + wave) * CW;  // this wave's chunks [c0, c0 + CW)
+    if (c0 >= chunks) return;
+    const int e = (int)(c0 / chunks_per_env);  // wave-uniform: scalar loads of the env's values
+    if (env_mask && !env_mask[e]) return;
+    bool night = is_night[e] != 0;  // the PRE-step is_night (see adv_observation_kernel)
+    if (time_step && p.day_length > 0 && time_step[e] % p.day_length == 0) night = !night;
+    const int64_t pcell = (int64_t)pos[2 * e] * W + pos[2 * e + 1];
+    const float4* colt = COL[night ? 1 : 0];
+    const uint8_t* dsrc = dousing ? dousing : grid;  // no dousing: read the grid again and mask it (no branch)
+    const uint32_t dmask = dousing ? ~0u : 0u;
+    uint32_t gw[CW], dw[CW];
+#pragma unroll
+    for (int i = 0; i < CW; ++i) {
+#ifdef GCA_OBS_ABL_NOREAD  // ablation (wrong results): no grid / dousing reads, the stores alone
+        gw[i] = (uint32_t)i;
+        dw[i] = 0u;
+#else
+        gw[i] = *reinterpret_cast<const uint32_t*>(grid + 256 * (c0 + i) + 4 * lane);
+        dw[i] = *reinterpret_cast<const uint32_t*>(dsrc + 256 * (c0 + i) + 4 * lane);
+#endif
+    }
+#pragma unroll
+    for (int i = 0; i < CW; ++i) {
+        const int64_t c = c0 + i;
+        const int64_t cell0 = 256 * (c - (int64_t)e * chunks_per_env) + 4 * lane;  // cell of this lane within the env
+        const uint32_t g4 = gw[i], d4 = dw[i] & dmask;
+        float out[12];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int v = (int)((g4 >> (8 * j)) & 0xFFu);
+            const int kind = colour_kind(p, v, cell0 + j == pcell);
+            const float4 cl = colt[3 * kind + (int)min((d4 >> (8 * j)) & 0xFFu, 2u)];
+            out[3 * j] = cl.x;
+            out[3 * j + 1] = cl.y;
+            out[3 * j + 2] = cl.z;
+        }
+        OUT4[3 * lane + 0] = make_float4(out[0], out[1], out[2], out[3]);
+        OUT4[3 * lane + 1] = make_float4(out[4], out[5], out[6], out[7]);
+        OUT4[3 * lane + 2] = make_float4(out[8], out[9], out[10], out[11]);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const float4 v0 = OUT4[lane], v1 = OUT4[lane + 64], v2 = OUT4[lane + 128];
+        f4v* dst = reinterpret_cast<f4v*>(rgb + 768 * c);
+        __builtin_nontemporal_store((f4v){v0.x, v0.y, v0.z, v0.w}, dst + lane);
+        __builtin_nontemporal_store((f4v){v1.x, v1.y, v1.z, v1.w}, dst + lane + 64);
+        __builtin_nontemporal_store((f4v){v2.x, v2.y, v2.z, v2.w}, dst + lane + 128);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // this chunk's LDS reads before the next one's writes
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
 }
 
 }  // namespace
@@ -435,12 +496,22 @@ extern "C" int gca_adv_observation(const gca_obs_params* p, int mode, int E, int
     GCA_CHECK_ARG(((uintptr_t)rgb & 15u) == 0 && ((uintptr_t)grid & 3u) == 0 && ((uintptr_t)dousing & 3u) == 0,
                   "adv_observation: rgb must be 16-B and grid/dousing 4-B aligned");
     // rows per block; (2 RB + 2) * W bytes of dynamic LDS (grid + dousing), at most 48 KiB
+    const int64_t HW = (int64_t)H * W;
+    constexpr int CWP = GCA_OBS_PLAIN;  // chunks of 256 cells per wave
+    if (CWP > 0 && mode == 0 && !p->enable_extensions && !p->should_transform && channels == nullptr &&
+        HW % 256 == 0 && (HW / 256) % (CWP > 0 ? CWP : 1) == 0) {
+        const int64_t chunks = (int64_t)E * (HW / 256);
+        const int64_t waves = chunks / (CWP > 0 ? CWP : 1);
+        hipLaunchKernelGGL(adv_obs_plain_kernel<(CWP > 0 ? CWP : 1)>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0,
+                           (hipStream_t)stream, *p, chunks, (int)(HW / 256), W, grid, dousing, pos, is_night, time_step,
+                           rgb, env_mask);
+        GCA_CHECK_LAUNCH("adv_obs_plain");
+        return GCA_OK;
+    }
     const int RB = max(1, min(GCA_OBS_RB, 24576 / W - 1));
     const int bpe = (H + RB - 1) / RB;
-    // blocks per workgroup: the production shape (step mode, W % 16 == 0) chains GCA_OBS_NB blocks of one env
-    const int nbw = (mode == 0 && W % 16 == 0 && bpe % GCA_OBS_NB == 0) ? GCA_OBS_NB : 1;
-    hipLaunchKernelGGL(adv_observation_kernel, dim3((unsigned)((int64_t)E * bpe / nbw)), dim3(256), (size_t)(2 * RB + 2) * W,
-                       (hipStream_t)stream, *p, mode, H, W, RB, bpe, nbw, grid, dousing, pos, is_night, time_step, action,
+    hipLaunchKernelGGL(adv_observation_kernel, dim3((unsigned)((int64_t)E * bpe)), dim3(256), (size_t)(2 * RB + 2) * W,
+                       (hipStream_t)stream, *p, mode, H, W, RB, bpe, grid, dousing, pos, is_night, time_step, action,
                        action_stride, rgb, channels, env_mask);
     GCA_CHECK_LAUNCH("adv_observation");
     return GCA_OK;

@@ -255,7 +255,7 @@ __global__ __launch_bounds__(256) void windy_fast_kernel(uint8_t* __restrict__ b
 #define GCA_WINDY_ROWS 1  // 0: the 16-cells-per-lane fast kernel for every W
 #endif
 #ifndef GCA_WINDY_RSH
-#define GCA_WINDY_RSH 32  // strip height per wave
+#define GCA_WINDY_RSH 16  // strip height per wave (r02j: 16 / 32 / 64 rows -> config 5 CA 105.9 / 109.7 / 110.5 us, config 2 equal)
 #endif
 #ifndef GCA_WINDY_RD
 #define GCA_WINDY_RD 8  // rows in flight ahead of the row being classified

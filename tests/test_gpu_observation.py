@@ -45,7 +45,8 @@ def make(E, H, W, seed, p3=0.0):
 
 
 @pytest.mark.parametrize("enable", [False, True])
-@pytest.mark.parametrize("E,H,W,seed", [(6, 8, 8, 0), (6, 16, 24, 1), (4, 64, 64, 2), (3, 37, 53, 3), (2, 256, 256, 4)])
+@pytest.mark.parametrize("E,H,W,seed", [(6, 8, 8, 0), (6, 16, 24, 1), (4, 64, 64, 2), (3, 37, 53, 3), (2, 256, 256, 4),
+                                        (5, 16, 48, 5), (7, 32, 8, 6)])
 def test_step_observation_matches_reference(device, enable, E, H, W, seed):
     from gymca_amd.forest_fire.bulldozer.observation import EXTENSION_LOOKUP, make_obs_params
 
