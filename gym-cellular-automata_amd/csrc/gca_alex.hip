@@ -904,7 +904,7 @@ __global__ __launch_bounds__(256, GCA_ALEX_WGS) void alex_step_kernel(
             const uint32_t n0 = (uint32_t)randint_ms(a0, p.age_lo, p.age_hi);
             const uint32_t n1 = (uint32_t)randint_ms(a1, p.age_lo, p.age_hi);
             NA[pp] = __builtin_amdgcn_perm(n1, n0, 0x05040100u);
-            __builtin_amdgcn_sched_barrier(0);  // one Philox block in flight per lane
+            __builtin_amdgcn_sched_barrier(0);  // one Philox block in flight per lane (2 or 4 interleaved: same time, r02h)
         }
         burn = (__builtin_bitreverse32(Dt) >> 16) & treeB & okB;
         grow = (__builtin_bitreverse32(Dg) >> 16) & emptyB & okB;
