@@ -628,7 +628,10 @@ __global__ __launch_bounds__(256, GCA_ALEX_WGS) void alex_step_kernel(
                 if (i & 1) {
                     const int j = i >> 1;
                     if (k <= R) ph2[j] = __builtin_elementwise_fma((f2){wk, wk}, (f2){fire_f(sprev), fire_f(s)}, ph2[j]);
-                    const f2 dsum = {(float)(sprev >> 16), (float)(s >> 16)};
+                    // PK: dousing is 0 / 1 per cell, so the D_1 / D_2 box sums are <= 25 and one v_cvt_f32_ubyte2 converts
+                    // them; the plain layouts' u8 counts can sum past 255 (full 16-bit field)
+                    const f2 dsum = PK ? (f2){(float)((sprev >> 16) & 0xFFu), (float)((s >> 16) & 0xFFu)}
+                                       : (f2){(float)(sprev >> 16), (float)(s >> 16)};
                     if (k == 1) dz2[j] = (f2){w_in_minus_bd, w_in_minus_bd} * dsum;
                     if (k == 2) dz2[j] = __builtin_elementwise_fma((f2){p.dous_border, p.dous_border}, dsum, dz2[j]);
                 }
