@@ -28,7 +28,11 @@
 
 namespace {
 
-constexpr int TH = 16;
+#ifndef GCA_ALEX_TH
+#define GCA_ALEX_TH 16  // tile rows (A/B hook: 32 rows = 512 threads, run with GCA_ALEX_WGS=2)
+#endif
+constexpr int TH = GCA_ALEX_TH;
+constexpr int NT = 16 * TH;  // threads per workgroup (16 lanes per image row)
 constexpr int TW = 256;
 constexpr int CW = TW + 32;  // staged columns: [c0-16, c0+TW+16)
 // LDS row layout of the column prefix: rows of CWP dwords, one 16-dword chunk per 16 columns (16-B
@@ -162,7 +166,7 @@ __host__ __device__ constexpr int cp_bytes(int RR, bool pk) {
     return (GCA_ALEX_GLDS && pk && 4 * (RR + 1) * CWP < 32768) ? 32768 : 4 * (RR + 1) * CWP;
 }
 template <int R, int MODE, bool FAST, bool ES, bool PK = false>
-__global__ __launch_bounds__(256, GCA_ALEX_WGS) void alex_step_kernel(
+__global__ __launch_bounds__(NT, GCA_ALEX_WGS) void alex_step_kernel(
     gca_alex_params p, int H, int W, int tiles_r, int tiles_c, const uint8_t* __restrict__ grid_in,
     uint8_t* __restrict__ grid_out, const int16_t* age_in, int16_t* age_out,  // no __restrict__: PK updates in place
     const uint8_t* __restrict__ veg, const uint8_t* __restrict__ den, const uint8_t* __restrict__ dousing,
@@ -358,11 +362,11 @@ __global__ __launch_bounds__(256, GCA_ALEX_WGS) void alex_step_kernel(
     // ---------------- stage rows [r0-RS, r0+TH+RS) x cols [c0-16, c0+TW+16):
     //                  packed fire | dousing<<16 -> CP rows 1..RR, fire bitmask -> FB
     //                  every load of the thread's chunks is issued before any is processed
-    constexpr int NIT = (RR * NCH + 255) / 256;
+    constexpr int NIT = (RR * NCH + NT - 1) / NT;
     uint32_t sgw[NIT][4], sdw[NIT][4];
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
-        const int ch = tid + 256 * it;
+        const int ch = tid + NT * it;
         const int sr = ch / NCH, cq = ch - sr * NCH;
         const int gr = r0 - RS + sr, gc = c0 - 16 + 16 * cq;
         uint32_t* gw = sgw[it];
@@ -451,7 +455,7 @@ __global__ __launch_bounds__(256, GCA_ALEX_WGS) void alex_step_kernel(
     int near_fire = 0;  // a FIRE cell within one row of the tile (rows r0-1 .. r0+TH) in this thread's chunks
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
-        const int ch = tid + 256 * it;
+        const int ch = tid + NT * it;
         if (ch >= RR * NCH) break;
         const int sr = ch / NCH, cq = ch - sr * NCH;
         uint32_t* cp = CP + (sr + 1) * CWP + 16 * cq;  // chunk cq; word j (columns 4j..4j+3) at slot (j + cq/4) & 3
@@ -470,7 +474,7 @@ __global__ __launch_bounds__(256, GCA_ALEX_WGS) void alex_step_kernel(
         FB[sr * NCH + cq] = (uint16_t)bits;
         near_fire |= (bits != 0u && sr >= RS - 1 && sr <= RS + TH) ? 1 : 0;
     }
-    for (int cc = tid; cc < CWP; cc += 256) CP[cc] = 0u;
+    for (int cc = tid; cc < CWP; cc += NT) CP[cc] = 0u;
     if (tid < 16) {
         const int v = tid & 7;
         // selects on the (SGPR) kernel arguments only: no dynamic indexing into the argument struct
@@ -535,7 +539,20 @@ __global__ __launch_bounds__(256, GCA_ALEX_WGS) void alex_step_kernel(
         }
     }
     // ---------------- column prefix: columns t and t + CW/2 per thread, every load before the adds
-    if (wg_need && tid < CW / 2) {
+    if constexpr (NT >= CW) {  // tall tiles: one column per thread
+        if (wg_need && tid < CW) {
+            const int pa = pcol(tid);
+            uint32_t va[RR];
+#pragma unroll
+            for (int k = 0; k < RR; ++k) va[k] = CP[(k + 1) * CWP + pa];
+            uint32_t ra = 0u;
+#pragma unroll
+            for (int k = 0; k < RR; ++k) {
+                ra += va[k];
+                CP[(k + 1) * CWP + pa] = ra;
+            }
+        }
+    } else if (wg_need && tid < CW / 2) {
         const int pa = pcol(tid), pb = pcol(tid + CW / 2);
         uint32_t va[RR], vb[RR];
 #pragma unroll
@@ -1023,13 +1040,13 @@ void launch_alex(const gca_alex_params& p, int E, int H, int W, const uint8_t* g
                       ((((uintptr_t)gi) | ((uintptr_t)go) | ((uintptr_t)ai) | ((uintptr_t)ao) | ((uintptr_t)veg) |
                         ((uintptr_t)den) | ((uintptr_t)dous) | ((uintptr_t)ps)) & 15u) == 0;
     if (PK)  // packed env layout (the host checked the FAST shape and alignment)
-        hipLaunchKernelGGL((alex_step_kernel<R, 0, true, true, true>), grid, dim3(256), lds, st, p, H, W, tiles_r,
+        hipLaunchKernelGGL((alex_step_kernel<R, 0, true, true, true>), grid, dim3(NT), lds, st, p, H, W, tiles_r,
                            tiles_c, gi, go, ai, ao, veg, den, dous, ps, wi, rs, ib, ig, ia, po, counts, act_in, act_out);
     else if (fast)  // production shape: no per-lane bounds checks (instantiated for the Philox mode only)
-        hipLaunchKernelGGL((alex_step_kernel<R, MODE, MODE == 0, ES>), grid, dim3(256), lds, st, p, H, W, tiles_r,
+        hipLaunchKernelGGL((alex_step_kernel<R, MODE, MODE == 0, ES>), grid, dim3(NT), lds, st, p, H, W, tiles_r,
                            tiles_c, gi, go, ai, ao, veg, den, dous, ps, wi, rs, ib, ig, ia, po, counts, act_in, act_out);
     else
-        hipLaunchKernelGGL((alex_step_kernel<R, MODE, false, ES>), grid, dim3(256), lds, st, p, H, W, tiles_r, tiles_c,
+        hipLaunchKernelGGL((alex_step_kernel<R, MODE, false, ES>), grid, dim3(NT), lds, st, p, H, W, tiles_r, tiles_c,
                            gi, go, ai, ao, veg, den, dous, ps, wi, rs, ib, ig, ia, po, counts, act_in, act_out);
 }
 
