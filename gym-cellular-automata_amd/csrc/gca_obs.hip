@@ -43,15 +43,6 @@
 #define GCA_OBS_PLAIN 1  // chunks of 256 cells per wave in adv_obs_plain_kernel (0: always the staged kernel; r02k with
                          // extensions off: 1 / 8 / 16 chunks -> 0.633 / 0.726 / 0.726 ms, staged kernel 0.688 ms)
 #endif
-#ifndef GCA_OBS_SEL
-#define GCA_OBS_SEL 0  // 1: adv_obs_sel_kernel (colours selected per lane from the kernel arguments, no block table)
-#endif
-#ifndef GCA_OBS_DIRECT
-#define GCA_OBS_DIRECT 0  // 1: adv_obs_direct_kernel (no LDS transposition, 768-B dwordx3 stores; A/B hook)
-#endif
-#ifndef GCA_OBS_STREAM
-#define GCA_OBS_STREAM 0  // > 0: adv_obs_stream_kernel with this many workgroups (A/B hook)
-#endif
 #ifndef GCA_OBS_NT
 #define GCA_OBS_NT 1  // non-temporal RGB stores (r01i A/B: 1.07 vs 1.10 ms per 4096 x 256^2)
 #endif
@@ -490,203 +481,6 @@ __global__ __launch_bounds__(256) void adv_obs_plain_kernel(gca_obs_params p, in
     }
 }
 
-// Streaming form of adv_obs_plain_kernel (GCA_OBS_STREAM > 0): a fixed grid of GCA_OBS_STREAM workgroups whose waves
-// walk the chunks with a stride of the total wave count, so at any moment the waves in flight write one contiguous
-// region of the frame (as a fill_ does) and the per-wave prologue (colour table, the env decode) is paid once per wave
-// instead of once per 3 KiB. The next chunk's grid / dousing dwords are loaded before the current chunk renders. The env
-// of a chunk is c >> cpe_shift when the chunks per env are a power of two (every W = 2^k grid), else a 32-bit divide.
-template <bool POW2>
-__global__ __launch_bounds__(256) void adv_obs_stream_kernel(gca_obs_params p, uint32_t chunks, uint32_t chunks_per_env,
-                                                             int cpe_shift, int W, const uint8_t* __restrict__ grid,
-                                                             const uint8_t* __restrict__ dousing,
-                                                             const int32_t* __restrict__ pos,
-                                                             const int32_t* __restrict__ is_night,
-                                                             const int32_t* __restrict__ time_step,
-                                                             float* __restrict__ rgb, const uint8_t* __restrict__ env_mask) {
-    __shared__ float4 COL[2][12];
-    __shared__ float4 OUT4s[4][192];
-    if (threadIdx.x < 24) {
-        float c3[3];
-        const int nt = (int)threadIdx.x / 12, i = (int)threadIdx.x % 12;
-        render_kind(p, c3, i / 3, i % 3, nt != 0);
-        COL[nt][i] = make_float4(c3[0], c3[1], c3[2], 0.0f);
-    }
-    __syncthreads();
-    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-    const uint32_t lane = threadIdx.x & 63u;
-    float4* OUT4 = OUT4s[wave];
-    typedef float f4v __attribute__((ext_vector_type(4)));
-    const uint32_t stride = gridDim.x * 4u;
-    uint32_t c = blockIdx.x * 4u + wave;
-    const uint8_t* dsrc = dousing ? dousing : grid;  // no dousing: read the grid again and mask it (no branch)
-    const uint32_t dmask = dousing ? ~0u : 0u;
-    uint32_t gw = 0u, dw = 0u;
-    if (c < chunks) {
-        gw = *reinterpret_cast<const uint32_t*>(grid + 256 * (size_t)c + 4 * lane);
-        dw = *reinterpret_cast<const uint32_t*>(dsrc + 256 * (size_t)c + 4 * lane);
-    }
-    for (; c < chunks; c += stride) {
-        const uint32_t cn = c + stride;
-        uint32_t gn = 0u, dn = 0u;
-        if (cn < chunks) {  // the next chunk's bytes fly while this one renders
-            gn = *reinterpret_cast<const uint32_t*>(grid + 256 * (size_t)cn + 4 * lane);
-            dn = *reinterpret_cast<const uint32_t*>(dsrc + 256 * (size_t)cn + 4 * lane);
-        }
-        const uint32_t e = POW2 ? (c >> cpe_shift) : (c / chunks_per_env);
-        if (!env_mask || env_mask[e]) {
-            bool night = is_night[e] != 0;  // the PRE-step is_night (see adv_observation_kernel)
-            if (time_step && p.day_length > 0 && time_step[e] % p.day_length == 0) night = !night;
-            const int64_t pcell = (int64_t)pos[2 * e] * W + pos[2 * e + 1];
-            const float4* colt = COL[night ? 1 : 0];
-            const int64_t cell0 = 256 * (int64_t)(c - e * chunks_per_env) + 4 * lane;
-            const uint32_t d4 = dw & dmask;
-            float out[12];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int v = (int)((gw >> (8 * j)) & 0xFFu);
-                const int kind = colour_kind(p, v, cell0 + j == pcell);
-                const float4 cl = colt[3 * kind + (int)min((d4 >> (8 * j)) & 0xFFu, 2u)];
-                out[3 * j] = cl.x;
-                out[3 * j + 1] = cl.y;
-                out[3 * j + 2] = cl.z;
-            }
-            OUT4[3 * lane + 0] = make_float4(out[0], out[1], out[2], out[3]);
-            OUT4[3 * lane + 1] = make_float4(out[4], out[5], out[6], out[7]);
-            OUT4[3 * lane + 2] = make_float4(out[8], out[9], out[10], out[11]);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            const float4 v0 = OUT4[lane], v1 = OUT4[lane + 64], v2 = OUT4[lane + 128];
-            f4v* dst = reinterpret_cast<f4v*>(rgb + 768 * (size_t)c);
-            __builtin_nontemporal_store((f4v){v0.x, v0.y, v0.z, v0.w}, dst + lane);
-            __builtin_nontemporal_store((f4v){v1.x, v1.y, v1.z, v1.w}, dst + lane + 64);
-            __builtin_nontemporal_store((f4v){v2.x, v2.y, v2.z, v2.w}, dst + lane + 128);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // this chunk's LDS reads before the next one's writes
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        }
-        gw = gn;
-        dw = dn;
-    }
-}
-
-// adv_obs_plain_kernel without the per-block colour table (GCA_OBS_SEL): each lane selects its cells' colours from the
-// kernel-argument colours (SGPR operands, static indices) with render_kind's own arithmetic, so a workgroup has no
-// barrier and no kernel-argument vector loads in front of its first store; the grid / dousing loads are issued first
-// and the env decode is a 32-bit divide.
-__device__ __forceinline__ void render_sel(const gca_obs_params& p, float* __restrict__ out, int kind, uint32_t dous,
-                                           bool night) {
-    const bool tinted = kind != 3 && dous > 0u;
-    const float s = dous == 1u ? 0.75f : 0.0f;
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-        const float c0 = night ? p.color_night[0][j] : p.color_day[0][j];
-        const float c1 = night ? p.color_night[1][j] : p.color_day[1][j];
-        const float c2 = night ? p.color_night[2][j] : p.color_day[2][j];
-        const float c3 = night ? p.color_night[3][j] : p.color_day[3][j];
-        const float t = night ? p.tint_night[j] : p.tint_day[j];
-        const float c = kind == 1 ? c1 : kind == 2 ? c2 : kind == 3 ? c3 : c0;
-        const float m = __fadd_rn(__fmul_rn(c, __fsub_rn(1.0f, s)), __fmul_rn(t, s));
-        out[j] = tinted ? m : c;
-    }
-}
-__global__ __launch_bounds__(256) void adv_obs_sel_kernel(gca_obs_params p, uint32_t chunks, uint32_t chunks_per_env,
-                                                          int W, const uint8_t* __restrict__ grid,
-                                                          const uint8_t* __restrict__ dousing,
-                                                          const int32_t* __restrict__ pos,
-                                                          const int32_t* __restrict__ is_night,
-                                                          const int32_t* __restrict__ time_step,
-                                                          float* __restrict__ rgb, const uint8_t* __restrict__ env_mask) {
-    __shared__ float4 OUT4s[4][192];
-    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6), lane = threadIdx.x & 63u;
-    const uint32_t c = blockIdx.x * 4u + wave;  // this wave's chunk of 256 cells
-    if (c >= chunks) return;
-    const uint8_t* dsrc = dousing ? dousing : grid;  // no dousing: read the grid again and mask it (no branch)
-    const uint32_t g4 = *reinterpret_cast<const uint32_t*>(grid + 256 * (size_t)c + 4 * lane);
-    const uint32_t d4 = *reinterpret_cast<const uint32_t*>(dsrc + 256 * (size_t)c + 4 * lane) & (dousing ? ~0u : 0u);
-    const uint32_t e = c / chunks_per_env;  // wave-uniform
-    if (env_mask && !env_mask[e]) return;
-    bool night = is_night[e] != 0;  // the PRE-step is_night (see adv_observation_kernel)
-    if (time_step && p.day_length > 0 && time_step[e] % p.day_length == 0) night = !night;
-    const int64_t pcell = (int64_t)pos[2 * e] * W + pos[2 * e + 1];
-    const int64_t cell0 = 256 * (int64_t)(c - e * chunks_per_env) + 4 * lane;
-    float out[12];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int kind = colour_kind(p, (int)((g4 >> (8 * j)) & 0xFFu), cell0 + j == pcell);
-        render_sel(p, out + 3 * j, kind, min((d4 >> (8 * j)) & 0xFFu, 2u), night);
-    }
-    float4* OUT4 = OUT4s[wave];
-    typedef float f4v __attribute__((ext_vector_type(4)));
-    OUT4[3 * lane + 0] = make_float4(out[0], out[1], out[2], out[3]);
-    OUT4[3 * lane + 1] = make_float4(out[4], out[5], out[6], out[7]);
-    OUT4[3 * lane + 2] = make_float4(out[8], out[9], out[10], out[11]);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const float4 v0 = OUT4[lane], v1 = OUT4[lane + 64], v2 = OUT4[lane + 128];
-    f4v* dst = reinterpret_cast<f4v*>(rgb + 768 * (size_t)c);
-    __builtin_nontemporal_store((f4v){v0.x, v0.y, v0.z, v0.w}, dst + lane);
-    __builtin_nontemporal_store((f4v){v1.x, v1.y, v1.z, v1.w}, dst + lane + 64);
-    __builtin_nontemporal_store((f4v){v2.x, v2.y, v2.z, v2.w}, dst + lane + 128);
-}
-
-// Direct form of adv_obs_plain_kernel (GCA_OBS_DIRECT): lane l of a wave renders cells l, l + 64, l + 128, l + 192 of
-// its 256-cell chunk, so each of its four RGB stores (one cell's 12 B, global_store_dwordx3) is one instruction writing
-// 768 contiguous bytes across the wave — no LDS transposition, no wave fences. Grid / dousing come in as byte loads
-// (64 contiguous bytes per instruction).
-__global__ __launch_bounds__(256) void adv_obs_direct_kernel(gca_obs_params p, int64_t chunks, int chunks_per_env, int W,
-                                                             const uint8_t* __restrict__ grid,
-                                                             const uint8_t* __restrict__ dousing,
-                                                             const int32_t* __restrict__ pos,
-                                                             const int32_t* __restrict__ is_night,
-                                                             const int32_t* __restrict__ time_step,
-                                                             float* __restrict__ rgb, const uint8_t* __restrict__ env_mask) {
-    __shared__ float4 COL[2][12];
-    if (threadIdx.x < 24) {
-        float c3[3];
-        const int nt = (int)threadIdx.x / 12, i = (int)threadIdx.x % 12;
-        render_kind(p, c3, i / 3, i % 3, nt != 0);
-        COL[nt][i] = make_float4(c3[0], c3[1], c3[2], 0.0f);
-    }
-    __syncthreads();
-    const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6), lane = (int)threadIdx.x & 63;
-    const uint32_t c = (uint32_t)blockIdx.x * 4u + (uint32_t)wave;  // this wave's chunk
-    if ((int64_t)c >= chunks) return;
-    const uint32_t e = c / (uint32_t)chunks_per_env;  // wave-uniform
-    if (env_mask && !env_mask[e]) return;
-    bool night = is_night[e] != 0;  // the PRE-step is_night (see adv_observation_kernel)
-    if (time_step && p.day_length > 0 && time_step[e] % p.day_length == 0) night = !night;
-    const int64_t pcell = (int64_t)pos[2 * e] * W + pos[2 * e + 1];
-    const float4* colt = COL[night ? 1 : 0];
-    const uint8_t* gsrc = grid + 256 * (size_t)c + lane;
-    // no dousing: read the grid again and mask it (no branch between the loads)
-    const uint8_t* dsrc = (dousing ? dousing : grid) + 256 * (size_t)c + lane;
-    const uint32_t dmask = dousing ? 0xFFu : 0u;
-    uint32_t g[4], d[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        g[j] = gsrc[64 * j];
-        d[j] = dsrc[64 * j];
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) d[j] &= dmask;
-    const int64_t cell0 = 256 * (int64_t)(c - e * (uint32_t)chunks_per_env) + lane;
-    float* dst = rgb + 768 * (size_t)c + 3 * lane;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int kind = colour_kind(p, (int)g[j], cell0 + 64 * j == pcell);
-        const float4 cl = colt[3 * kind + (int)min(d[j], 2u)];
-        typedef float f3v __attribute__((ext_vector_type(3)));
-        f3v v = {cl.x, cl.y, cl.z};
-#if GCA_OBS_NT
-        __builtin_nontemporal_store(v, reinterpret_cast<f3v*>(dst + 192 * j));
-#else
-        *reinterpret_cast<f3v*>(dst + 192 * j) = v;
-#endif
-    }
-}
-
 }  // namespace
 
 extern "C" int gca_adv_observation(const gca_obs_params* p, int mode, int E, int H, int W, const uint8_t* grid,
@@ -704,37 +498,6 @@ extern "C" int gca_adv_observation(const gca_obs_params* p, int mode, int E, int
     // rows per block; (2 RB + 2) * W bytes of dynamic LDS (grid + dousing), at most 48 KiB
     const int64_t HW = (int64_t)H * W;
     constexpr int CWP = GCA_OBS_PLAIN;  // chunks of 256 cells per wave
-    if (GCA_OBS_SEL && mode == 0 && !p->enable_extensions && !p->should_transform && channels == nullptr &&
-        HW % 256 == 0 && (int64_t)E * (HW / 256) < (int64_t)UINT32_MAX - 4) {
-        const uint32_t chunks = (uint32_t)((int64_t)E * (HW / 256));
-        hipLaunchKernelGGL(adv_obs_sel_kernel, dim3((chunks + 3u) / 4u), dim3(256), 0, (hipStream_t)stream, *p, chunks,
-                           (uint32_t)(HW / 256), W, grid, dousing, pos, is_night, time_step, rgb, env_mask);
-        GCA_CHECK_LAUNCH("adv_obs_sel");
-        return GCA_OK;
-    }
-    if (GCA_OBS_DIRECT && mode == 0 && !p->enable_extensions && !p->should_transform && channels == nullptr &&
-        HW % 256 == 0 && (int64_t)E * (HW / 256) < (int64_t)UINT32_MAX) {
-        const int64_t chunks = (int64_t)E * (HW / 256);
-        hipLaunchKernelGGL(adv_obs_direct_kernel, dim3((unsigned)((chunks + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
-                           *p, chunks, (int)(HW / 256), W, grid, dousing, pos, is_night, time_step, rgb, env_mask);
-        GCA_CHECK_LAUNCH("adv_obs_direct");
-        return GCA_OK;
-    }
-    if (GCA_OBS_STREAM > 0 && mode == 0 && !p->enable_extensions && !p->should_transform && channels == nullptr &&
-        HW % 256 == 0 && (int64_t)E * (HW / 256) < (int64_t)UINT32_MAX - (int64_t)GCA_OBS_STREAM * 4) {
-        const uint32_t chunks = (uint32_t)((int64_t)E * (HW / 256)), cpe = (uint32_t)(HW / 256);
-        const int shift = __builtin_ctz(cpe);
-        const int64_t need = ((int64_t)chunks + 3) / 4;
-        const unsigned blocks = (unsigned)(need < GCA_OBS_STREAM ? need : GCA_OBS_STREAM);
-        if ((cpe & (cpe - 1)) == 0)
-            hipLaunchKernelGGL(adv_obs_stream_kernel<true>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p, chunks,
-                               cpe, shift, W, grid, dousing, pos, is_night, time_step, rgb, env_mask);
-        else
-            hipLaunchKernelGGL(adv_obs_stream_kernel<false>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p, chunks,
-                               cpe, shift, W, grid, dousing, pos, is_night, time_step, rgb, env_mask);
-        GCA_CHECK_LAUNCH("adv_obs_stream");
-        return GCA_OK;
-    }
     if (CWP > 0 && mode == 0 && !p->enable_extensions && !p->should_transform && channels == nullptr &&
         HW % 256 == 0 && (HW / 256) % (CWP > 0 ? CWP : 1) == 0) {
         const int64_t chunks = (int64_t)E * (HW / 256);
