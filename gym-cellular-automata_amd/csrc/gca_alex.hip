@@ -156,6 +156,9 @@ template <class T, class S> __device__ __forceinline__ T bitcast_(S s) {
 // loads are all retired before the first of them (the ties at the end of the heat phase). Bit-exact (the packed-kernel
 // GPU tests), but 2 % SLOWER on the headline (r02h: 1.460 vs 1.433 ms; profiles/r02h), so it stays off: more slope
 // bytes in flight is not what bounds the step.
+#ifndef GCA_ALEX_PRIO
+#define GCA_ALEX_PRIO 0  // A/B hook: 1 = wave priority 3 while a tile issues its staging loads, 0 after; 2 = also 3 for the stores
+#endif
 #ifndef GCA_ALEX_GLDS
 #define GCA_ALEX_GLDS 0
 #endif
@@ -203,6 +206,7 @@ __global__ __launch_bounds__(NT, GCA_ALEX_WGS) void alex_step_kernel(
     const uint16_t* dbE = reinterpret_cast<const uint16_t*>(dousing) + (int64_t)e * (HW >> 4);  // PK: dousing bits
     static_assert(!PK || (ES && FAST && MODE == 0), "packed layout: edge slopes, FAST shape, Philox mode");
     const int tid = threadIdx.x;
+    if (GCA_ALEX_PRIO) __builtin_amdgcn_s_setprio(3);  // (A/B hook) issue this tile's loads ahead of other waves' compute
     const bool rows16 = FAST || (((W & 15) == 0) &&
                                  ((((uintptr_t)grid_in) | ((uintptr_t)dousing) | ((uintptr_t)grid_out) |
                                    ((uintptr_t)veg) | ((uintptr_t)den) | ((uintptr_t)age_in) | ((uintptr_t)age_out) |
@@ -452,6 +456,7 @@ __global__ __launch_bounds__(NT, GCA_ALEX_WGS) void alex_step_kernel(
         }
         if (tid == 0) act_out[(size_t)e * tiles_all + tile] = 0;
     }
+    if (GCA_ALEX_PRIO) __builtin_amdgcn_s_setprio(0);
     int near_fire = 0;  // a FIRE cell within one row of the tile (rows r0-1 .. r0+TH) in this thread's chunks
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
@@ -976,6 +981,7 @@ __global__ __launch_bounds__(NT, GCA_ALEX_WGS) void alex_step_kernel(
     }
 
     // ---------------- stores
+    if (GCA_ALEX_PRIO >= 2) __builtin_amdgcn_s_setprio(3);  // (A/B hook) finish and free the slot
     if (vec) {
         uint8_t* gEo = grid_out + (size_t)e * HW;
         int16_t* aEo = age_out + (size_t)e * HW;
