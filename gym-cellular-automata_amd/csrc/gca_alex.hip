@@ -157,7 +157,13 @@ template <class T, class S> __device__ __forceinline__ T bitcast_(S s) {
 // GPU tests), but 2 % SLOWER on the headline (r02h: 1.460 vs 1.433 ms; profiles/r02h), so it stays off: more slope
 // bytes in flight is not what bounds the step.
 #ifndef GCA_ALEX_PRIO
-#define GCA_ALEX_PRIO 0  // A/B hook: 1 = wave priority 3 while a tile issues its staging loads, 0 after; 2 = also 3 for the stores
+// Wave priorities (s_setprio) along a tile's phase chain. Default 5: 3 while a tile issues its staging loads, 2 through
+// the LDS writes and the column prefix (the phases in front of the workgroup's last barrier), 0 from the heat phase on,
+// so the SIMD arbiter lets waves that hold up a barrier issue ahead of the barrier-free heat / slope / Philox work of the
+// other workgroups. r02r (profiles/r02r): 1.405 vs 1.434 ms (-2.0 %) on the headline, +4 % on the sparse episode-start
+// state; other levels: 1 = 3 for the staging loads then 0 (-0.6 %); 2 = 1 + 3 for the stores (-0.6 %); 3 = 2 + the
+// direction pass at 2 above the heat phase (+21 %); 4 = 5 with the heat phase at 1 (+1 %); 0 = off.
+#define GCA_ALEX_PRIO 5
 #endif
 #ifndef GCA_ALEX_GLDS
 #define GCA_ALEX_GLDS 0
@@ -456,7 +462,7 @@ __global__ __launch_bounds__(NT, GCA_ALEX_WGS) void alex_step_kernel(
         }
         if (tid == 0) act_out[(size_t)e * tiles_all + tile] = 0;
     }
-    if (GCA_ALEX_PRIO) __builtin_amdgcn_s_setprio(0);
+    if (GCA_ALEX_PRIO) __builtin_amdgcn_s_setprio(GCA_ALEX_PRIO >= 4 ? 2 : 0);
     int near_fire = 0;  // a FIRE cell within one row of the tile (rows r0-1 .. r0+TH) in this thread's chunks
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
@@ -575,6 +581,7 @@ __global__ __launch_bounds__(NT, GCA_ALEX_WGS) void alex_step_kernel(
         }
     }
     __syncthreads();
+    if (GCA_ALEX_PRIO >= 4) __builtin_amdgcn_s_setprio(GCA_ALEX_PRIO == 4 ? 1 : 0);  // past the last barrier
 
     __builtin_amdgcn_sched_barrier(0);
 
@@ -724,6 +731,7 @@ __global__ __launch_bounds__(NT, GCA_ALEX_WGS) void alex_step_kernel(
 #pragma unroll
     for (int j = 0; j < 8; ++j) qn2[j] = (f2){1.0f, 1.0f};
     uint32_t burn_inj = 0u;
+    if (GCA_ALEX_PRIO >= 3) __builtin_amdgcn_s_setprio(GCA_ALEX_PRIO == 3 ? 2 : 0);  // (A/B hook) slope-streaming pass
     if (wave_need) {
         // ---- base = (p_h * (1 + p_veg)) * (1 + p_den)   (left-to-right product of :206), clip(idx, 1, 5)
         //      (:176-178) through the LDS table
@@ -880,6 +888,7 @@ __global__ __launch_bounds__(NT, GCA_ALEX_WGS) void alex_step_kernel(
         load_ages();
     }
 
+    if (GCA_ALEX_PRIO == 3) __builtin_amdgcn_s_setprio(0);
     // ---- draws: burn / grow masks and the packed new-fire ages NA (two cells per word)
     uint32_t burn, grow, NA[8];
     if (INJECT) {
@@ -981,7 +990,7 @@ __global__ __launch_bounds__(NT, GCA_ALEX_WGS) void alex_step_kernel(
     }
 
     // ---------------- stores
-    if (GCA_ALEX_PRIO >= 2) __builtin_amdgcn_s_setprio(3);  // (A/B hook) finish and free the slot
+    if (GCA_ALEX_PRIO == 2 || GCA_ALEX_PRIO == 3) __builtin_amdgcn_s_setprio(3);  // (A/B hook) finish and free the slot
     if (vec) {
         uint8_t* gEo = grid_out + (size_t)e * HW;
         int16_t* aEo = age_out + (size_t)e * HW;
