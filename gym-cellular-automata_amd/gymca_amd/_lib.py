@@ -11,6 +11,8 @@ from ctypes import POINTER, c_double, c_float, c_int, c_int16, c_int32, c_int64,
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # GCA_LIB_PATH: an alternative build of the same library (A/B kernel experiments, scripts/build_variant.sh)
 LIB_PATH = os.environ.get("GCA_LIB_PATH") or os.path.join(_HERE, "_lib", "libgca_hip.so")
+# the host backend of the same C-ABI (csrc/gca_cpu.cpp): host pointers, `stream` ignored
+CPU_LIB_PATH = os.path.join(_HERE, "_lib", "libgca_cpu.so")
 
 GCA_OK = 0
 GCA_MAX_RADIUS = 8
@@ -208,8 +210,12 @@ _SIGNATURES = {
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGNATURES)
+# the subset libgca_cpu.so exports (tiny grids and the O(1)-per-env operators on host arrays)
+CPU_SYMBOLS = ("gca_last_error", "gca_version", "gca_philox", "gca_count_cells", "gca_move_modify",
+               "gca_ds_count_draws", "gca_ds_step")
 
 _lib = None
+_lib_cpu = None
 
 
 def load():
@@ -229,6 +235,36 @@ def load():
         fn.restype = restype
     _lib = lib
     return lib
+
+
+def load_cpu():
+    """Load libgca_cpu.so once; raise GCAError if it is not built."""
+    global _lib_cpu
+    if _lib_cpu is not None:
+        return _lib_cpu
+    if not os.path.exists(CPU_LIB_PATH):
+        raise GCAError(f"{CPU_LIB_PATH} not found: build it with `make -C gym-cellular-automata_amd/csrc`")
+    lib = ctypes.CDLL(CPU_LIB_PATH, mode=ctypes.RTLD_LOCAL)
+    for name in CPU_SYMBOLS:
+        fn = getattr(lib, name)
+        fn.argtypes, fn.restype = _SIGNATURES[name]
+    _lib_cpu = lib
+    return lib
+
+
+_cpu_fns = {}
+
+
+def call_cpu(name, *args):
+    """Call a gca_* entry point of the host backend (host pointers) and raise GCAError on a non-zero status."""
+    fn = _cpu_fns.get(name)
+    if fn is None:
+        fn = _cpu_fns[name] = getattr(load_cpu(), name)
+    status = fn(*args)
+    if status != GCA_OK:
+        msg = _lib_cpu.gca_last_error().decode(errors="replace")
+        raise GCAError(f"{name} (host backend) failed (status {status}): {msg}")
+    return status
 
 
 def call(name, *args):

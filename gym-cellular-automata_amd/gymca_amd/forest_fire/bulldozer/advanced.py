@@ -139,6 +139,7 @@ class AdvancedForestFireBulldozerEnv:
         self.truncated = torch.zeros(E, dtype=torch.bool, **kw)  # the reference never truncates (:392)
         self._winds_dev = torch.as_tensor(self._winds, device=self.device)
         self._initial = None
+        self._mdp = None
         if observation not in ("grid", "rgb"):
             raise ValueError("observation must be 'grid' or 'rgb'")
         if observation == "rgb" and H != W:
@@ -357,6 +358,33 @@ class AdvancedForestFireBulldozerEnv:
                   "p_wind_change": self._p_wind_change, "day_length": self._day_length}
         return {"per_env_context": per_env, "shared_context": shared, "position": self.pos, "time": self.accu}
 
+    def reference_context(self):
+        """The context in the reference's own layout (advanced_bulldozer.py:109-129, :711-743), materialised on the
+        device: true_grid / fire_age f32, density / vegetation / dousing_count / wind_index / time_step / is_night
+        int32, altitude f64, slope (E, H, W, 3, 3) f32 (get_slope of the altitude; zeros without one), "key" the
+        per-env Philox step counter. For callers of env.MDP.update or code that reads the reference's keys; the
+        step itself keeps the compact layout of _context()."""
+        import torch
+
+        E, H, W = self.num_envs, self.nrows, self.ncols
+        i32 = torch.int32
+        slope = torch.zeros((E, H, W, 3, 3), dtype=torch.float32, device=self.device)
+        alt = self.altitude if self.altitude is not None else torch.zeros((E, H, W), dtype=torch.float64,
+                                                                          device=self.device)
+        if self.altitude is not None:
+            tmp = torch.empty((E, 8, H, W), dtype=torch.float32, device=self.device)
+            call("gca_alex_slope_from_altitude", dev.ptr(self.altitude), dev.ptr(tmp), dev.ptr(slope), E, H, W,
+                 dev.stream_ptr(self.device))
+        per_env = {"wind_index": self.wind_index.clone(), "density": self.density.to(i32),
+                   "vegetation": self.vegetation.to(i32), "altitude": alt.clone(), "slope": slope,
+                   "fire_age": self.age[self.cur].to(torch.float32), "key": self.rng_step.clone(),
+                   "is_night": self.is_night.clone(), "true_grid": self.grid[self.cur].to(torch.float32),
+                   "time_step": self.time_step.clone(), "dousing_count": self.dousing.to(i32)}
+        shared = {"winds": self._winds_dev, "p_fire": self._p_fire, "p_tree": self._p_tree,
+                  "p_wind_change": self._p_wind_change, "day_length": self._day_length}
+        return {"per_env_context": per_env, "shared_context": shared, "position": self.pos.clone(),
+                "time": self.accu.clone()}
+
     def _obs(self):
         return (self.rgb if self.rgb is not None else self.grid[self.cur]), self._context()
 
@@ -364,55 +392,197 @@ class AdvancedForestFireBulldozerEnv:
         return {"reward": self.reward, "terminated": self.done.bool(), "TimeLimit.truncated": self.truncated,
                 "steps_elapsed": self.steps_elapsed, "reward_accumulated": self.reward_accumulated}
 
+    @property
+    def MDP(self):
+        """The per-env MDP operator (advanced_bulldozer.py:66-68, 956-1133) wired to this env:
+        MDP.update(grid, action, per_env_context, shared_context, position, time) on the reference's context
+        layout, one env or a leading env axis (stateless_step's vmap). See advanced_mdp.py."""
+        if self._mdp is None:
+            from .advanced_mdp import make_env_mdp
+
+            self._mdp = make_env_mdp(self)
+        return self._mdp
+
+    def _is_own(self, x, buf):
+        return (dev.is_device_tensor(x) and x.data_ptr() == buf.data_ptr() and x.dtype == buf.dtype
+                and tuple(x.shape) == tuple(buf.shape))
+
     def _adopt(self, obs=None, info=None):
         """Make the env's device state the one `obs` / `info` describe (the functional reference threads state
-        through them, :332-399). Values that are this env's own buffers are skipped (zero cost in the usual
-        loop that passes back what the last call returned); anything else is copied in."""
+        through them, :332-399). Values that are this env's own buffers are skipped (zero cost in the usual loop
+        that passes back what the last call returned); anything else is validated first — nothing is written
+        when any value is refused — and then copied in. Honoured beyond the step state: a foreign "slope" (the
+        env's own layout, or the reference's (E, H, W, 3, 3) / (E, H, W, 9), which switches the env to the general
+        8-plane layout), "altitude" (carried, unread by the step as in the reference) and the shared context's
+        "winds", "p_tree", "p_wind_change" and "day_length". Refused with ValueError: shapes that match neither
+        layout, non-integer or out-of-range cell codes / fire ages, dousing counts > 1 on the packed layout."""
         import torch
 
-        touched = set()
+        E, H, W = self.num_envs, self.nrows, self.ncols
+        plan = []  # (name, source tensor on the device, destination buffer)
 
-        def load(x, buf, name):
-            if x is None:
+        def src_of(x, name, buf, integral=None):
+            if x is None or self._is_own(x, buf):
                 return
-            if dev.is_device_tensor(x) and x.data_ptr() == buf.data_ptr() and x.dtype == buf.dtype \
-                    and tuple(x.shape) == tuple(buf.shape):
-                return
-            src = x if dev.is_device_tensor(x) else torch.as_tensor(np.asarray(x))
-            if tuple(src.shape) != tuple(buf.shape):
-                raise ValueError(f"{name}: shape {tuple(src.shape)} does not match the env's {tuple(buf.shape)}")
-            buf.copy_(src.to(device=self.device, dtype=buf.dtype))
-            touched.add(name)
+            t = x if dev.is_device_tensor(x) else torch.as_tensor(np.asarray(x))
+            if tuple(t.shape) != tuple(buf.shape):
+                raise ValueError(f"{name}: shape {tuple(t.shape)} does not match the env's {tuple(buf.shape)}")
+            t = t.to(self.device)
+            if integral is not None and t.numel():
+                lo, hi = integral
+                if t.is_floating_point() and not bool(torch.equal(t, torch.round(t))):
+                    raise ValueError(f"{name}: values must be integers (the reference's states are integer-valued)")
+                if bool((t < lo).any()) or bool((t > hi).any()):
+                    raise ValueError(f"{name}: values outside [{lo}, {hi}] do not fit the env's layout")
+            plan.append((name, t, buf))
 
+        slope_src = altitude_src = None
+        shared = {}
         if obs is not None:
             ctx = obs[1]
             pe = ctx.get("per_env_context", {})
-            load(pe.get("true_grid"), self.grid[self.cur], "true_grid")
-            load(pe.get("fire_age"), self.age[self.cur], "fire_age")
-            load(pe.get("dousing_count"), self.dousing, "dousing_count")
-            load(pe.get("vegetation"), self.vegetation, "vegetation")
-            load(pe.get("density"), self.density, "density")
-            load(pe.get("wind_index"), self.wind_index, "wind_index")
-            load(pe.get("is_night"), self.is_night, "is_night")
-            load(pe.get("time_step"), self.time_step, "time_step")
-            load(pe.get("key"), self.rng_step, "key")
-            load(ctx.get("position"), self.pos, "position")
-            load(ctx.get("time"), self.accu, "time")
+            src_of(pe.get("true_grid"), "true_grid", self.grid[self.cur], (0, 255))
+            src_of(pe.get("fire_age"), "fire_age", self.age[self.cur], (-32768, 32767))
+            dous_hi = 1 if self.dous_bits is not None else 255
+            src_of(pe.get("dousing_count"), "dousing_count", self.dousing, (0, dous_hi))
+            src_of(pe.get("vegetation"), "vegetation", self.vegetation, (0, 255))
+            src_of(pe.get("density"), "density", self.density, (0, 255))
+            src_of(pe.get("wind_index"), "wind_index", self.wind_index, (0, len(self._winds) - 1))
+            src_of(pe.get("is_night"), "is_night", self.is_night, (0, 1))
+            src_of(pe.get("time_step"), "time_step", self.time_step)
+            src_of(pe.get("key"), "key", self.rng_step)
+            src_of(ctx.get("position"), "position", self.pos)
+            src_of(ctx.get("time"), "time", self.accu)
             if obs[0] is not None and self.rgb is not None:
-                load(obs[0], self.rgb, "rgb")
+                src_of(obs[0], "rgb", self.rgb)
+            slope_src = self._slope_source(pe.get("slope"))
+            alt = pe.get("altitude")
+            if alt is not None and not (self.altitude is not None and self._is_own(alt, self.altitude)):
+                a = alt if dev.is_device_tensor(alt) else torch.as_tensor(np.asarray(alt))
+                if tuple(a.shape) != (E, H, W):
+                    raise ValueError(f"altitude: shape {tuple(a.shape)} is not ({E}, {H}, {W})")
+                altitude_src = a
+            shared = self._shared_changes(ctx.get("shared_context"))
         if info is not None:
-            load(info.get("steps_elapsed"), self.steps_elapsed, "steps_elapsed")
-            load(info.get("reward_accumulated"), self.reward_accumulated, "reward_accumulated")
-            load(info.get("reward"), self.reward, "reward")
+            src_of(info.get("steps_elapsed"), "steps_elapsed", self.steps_elapsed)
+            src_of(info.get("reward_accumulated"), "reward_accumulated", self.reward_accumulated)
+            src_of(info.get("reward"), "reward", self.reward)
+        # everything validated: apply
+        touched = set()
+        for name, t, buf in plan:
+            buf.copy_(t.to(dtype=buf.dtype))
+            touched.add(name)
+        if altitude_src is not None:  # carried like the reference's context; the step reads the slopes only
+            self.altitude = altitude_src.to(self.device, torch.float64).contiguous().clone()
+        if slope_src is not None:
+            self._adopt_slope(*slope_src)
+        if shared:
+            self._apply_shared(shared)
         if {"vegetation", "density", "dousing_count"} & touched:
-            if self.dous_bits is not None and bool((self.dousing > 1).any()):
-                raise ValueError("the packed layout stores dousing counts as bits: values must be 0/1")
             self._pack_layers()
         if "true_grid" in touched:
             if self.act is not None:
                 self.act.fill_(1)
             call("gca_count_cells", dev.ptr(self.grid[self.cur]), self.num_envs, self.nrows, self.ncols, self._empty,
                  self._tree, self._fire, dev.ptr(self.counts), dev.stream_ptr(self.device))
+
+    def _slope_source(self, x):
+        """None (own buffer / absent) or (kind, tensor): kind "env" = this env's slope layout, "ref" = the
+        reference's f32 slopes (E, H, W, 9)."""
+        import torch
+
+        if x is None or self._is_own(x, self.slope_data):
+            return None
+        E, H, W = self.num_envs, self.nrows, self.ncols
+        t = x if dev.is_device_tensor(x) else torch.as_tensor(np.asarray(x))
+        shp = tuple(t.shape)
+        if shp == tuple(self.slope_data.shape):
+            return "env", t.to(self.device, torch.float32).contiguous()
+        if shp in ((E, H, W, 3, 3), (E, H, W, 9)):
+            t = t.to(self.device, torch.float32).reshape(E, H, W, 9).contiguous()
+            if bool((t.abs() > 90).any()):
+                raise ValueError("slope: degrees outside [-90, 90] (the reference's slope space)")
+            return "ref", t
+        raise ValueError(f"slope: shape {shp} is neither the env's layout {tuple(self.slope_data.shape)} nor the "
+                         f"reference's ({E}, {H}, {W}, 3, 3)")
+
+    def _adopt_slope(self, kind, t):
+        import torch
+
+        if kind == "env":
+            self.slope_data.copy_(t)
+            return
+        # arbitrary slopes need the general layout: 8 p_slope planes (gca_alex_step, 41 B per cell-update)
+        if self.slope_layout != "planes":
+            self._to_planes_layout()
+        E, H, W = self.num_envs, self.nrows, self.ncols
+        call("gca_alex_prepare_slope", dev.ptr(t), dev.ptr(self.slope_data), E, H, W, dev.stream_ptr(self.device))
+
+    def _to_planes_layout(self):
+        """Switch the step to the 8-plane p_slope layout (gca_alex_step) keeping the state: separate age buffers,
+        no packed vd / dousing bits / tile map."""
+        import torch
+
+        E, H, W = self.num_envs, self.nrows, self.ncols
+        ages = torch.zeros((2, E, H, W), dtype=torch.int16, device=self.device)
+        ages[self.cur].copy_(self.age[self.cur])
+        self.age = ages
+        self.slope_data = torch.zeros((E, 8, H, W), dtype=torch.float32, device=self.device)
+        self.slope_layout = "planes"
+        self.vd = self.dous_bits = self.act = None
+
+    def _shared_changes(self, sc):
+        """The shared-context values that differ from the env's (validated, not yet applied)."""
+        if not sc:
+            return {}
+        out = {}
+        w = sc.get("winds")
+        if w is not None and w is not self._winds_dev:
+            wn = (w.cpu().numpy() if dev.is_device_tensor(w) else np.asarray(w)).astype(np.float32)
+            if wn.ndim != 4 or wn.shape[1:] != (2, 3, 3) or not 1 <= wn.shape[0] <= 16:
+                raise ValueError("winds: expected (n, 2, 3, 3) with 1 <= n <= 16 (wind matrix, ft pairs)")
+            if not np.array_equal(wn, self._winds):
+                out["winds"] = wn
+        for k, cur in (("p_tree", self._p_tree), ("p_wind_change", self._p_wind_change),
+                       ("day_length", self._day_length)):
+            v = sc.get(k)
+            if v is None:
+                continue
+            v = float(v.item()) if dev.is_device_tensor(v) else float(np.asarray(v))
+            if v != cur:
+                if k == "day_length" and (v != int(v) or v < 1):
+                    raise ValueError("day_length must be a positive integer")
+                out[k] = v
+        return out
+
+    def _apply_shared(self, ch):
+        import torch
+
+        if "winds" in ch:
+            w = ch["winds"]
+            if len(w) <= int(self.wind_index.max().item()):
+                raise ValueError("winds: fewer wind matrices than the current wind indices need")
+            self._winds = w
+            self._winds_dev = torch.as_tensor(w, device=self.device)
+            self.alex_params.n_winds = self.env_params.n_winds = len(w)
+            for i, m in enumerate(w[:, 0]):
+                for j in range(9):
+                    self.alex_params.winds[i][j] = float(m.reshape(9)[j])
+            if self.pinecones:
+                from ..operators.pinecones import s_cdf_tables
+
+                self.pine_tables = torch.as_tensor(s_cdf_tables(w).view(np.int32), device=self.device)
+        if "p_tree" in ch:
+            self._p_tree = ch["p_tree"]
+            self.alex_params.p_tree = float(np.float32(ch["p_tree"]))
+        if "p_wind_change" in ch:
+            self._p_wind_change = ch["p_wind_change"]
+            self.env_params.p_wind_change = float(np.float32(ch["p_wind_change"]))
+        if "day_length" in ch:
+            self._day_length = int(ch["day_length"])
+            self.env_params.day_length = self._day_length
+            self.obs_params.day_length = self._day_length
+        self._mdp = None
 
     def _full_action(self, action):
         import torch

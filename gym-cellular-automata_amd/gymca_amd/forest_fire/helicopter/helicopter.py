@@ -1,15 +1,19 @@
 """ForestFireHelicopterEnv — drop-in for the reference env (helicopter.py:20-236).
 
 The Drossel–Schwabl CA (gca_ds_step), Move/Modify (gca_move_modify) and the reward
-cell counts (gca_count_cells) run on the GPU; the freeze countdown is host logic.
+cell counts (gca_count_cells) run in libgca_hip.so, or — for grids of at most HOST_MAX_CELLS cells, BASELINE
+config 1's 5x5 — in the host build of the same C-ABI (libgca_cpu.so, gymca_amd/_backend.py); `backend=` pins
+one. The freeze countdown is host logic.
 """
+from collections import Counter
 from typing import Optional
 
 import numpy as np
 
+from ... import _backend
 from ... import _device as dev
 from ..._config import TYPE_BOX, TYPE_INT
-from ..._lib import call
+from ..._lib import call, call_cpu
 from ...ca_env import CAEnv
 from ...grid_space import GridSpace
 from ...operator import Operator
@@ -37,8 +41,10 @@ class ForestFireHelicopterEnv(CAEnv):
         self._resample_initial = False
         return self._initial_state
 
-    def __init__(self, nrows, ncols, speed: float = 0.5, freeze: Optional[int] = None, **kwargs):
+    def __init__(self, nrows, ncols, speed: float = 0.5, freeze: Optional[int] = None, backend=None, **kwargs):
         super().__init__(nrows, ncols, **kwargs)
+        self.backend = backend
+        self._scratch = _backend.Scratch()
         self.title = "ForestFireHelicopter" + str(nrows) + "x" + str(ncols)
         self._n_actions = 9
         self._reward_per_empty, self._reward_per_tree, self._reward_per_fire = 0.0, 1.0, -1.0
@@ -50,9 +56,9 @@ class ForestFireHelicopterEnv(CAEnv):
         self._action_sets = {"up": {0, 1, 2}, "down": {6, 7, 8}, "left": {0, 3, 6}, "right": {2, 5, 8},
                              "not_move": {4}}
         self._set_spaces()
-        self.cellular_automaton = ForestFire(self._empty, self._tree, self._fire, **self.ca_space)
-        self.move = Move(self._action_sets, **self.move_space)
-        self.modify = Modify(self._effects, **self.modify_space)
+        self.cellular_automaton = ForestFire(self._empty, self._tree, self._fire, backend=backend, **self.ca_space)
+        self.move = Move(self._action_sets, backend=backend, **self.move_space)
+        self.modify = Modify(self._effects, backend=backend, **self.modify_space)
         self.move_modify = MoveModify(self.move, self.modify, **self.move_modify_space)
         self._MDP = MDP(self.cellular_automaton, self.move_modify, self._max_freeze, **self.MDP_space)
 
@@ -61,9 +67,11 @@ class ForestFireHelicopterEnv(CAEnv):
 
     def count_cells(self, grid=None):
         import torch
-        from collections import Counter
 
         grid = self.grid if grid is None else grid
+        if _backend.choose(self.backend, dev.is_device_tensor(grid), self.nrows * self.ncols) == "cpu":
+            c = self._host_counts(grid)
+            return Counter({v: int(n) for v, n in zip((self._empty, self._tree, self._fire), c) if n})
         device = dev.require_device()
         g = dev.to_device(np.asarray(grid).astype(np.uint8), torch.uint8, device)
         counts = torch.empty(3, dtype=torch.int32, device=device)
@@ -72,11 +80,21 @@ class ForestFireHelicopterEnv(CAEnv):
         c = counts.cpu().numpy().tolist()
         return Counter({v: n for v, n in zip((self._empty, self._tree, self._fire), c) if n})
 
+    def _host_counts(self, grid):
+        g, p_g = self._scratch.get("grid", (self.nrows, self.ncols), np.uint8)
+        c, p_c = self._scratch.get("counts", (3,), np.int32)
+        np.copyto(g, grid, casting="unsafe")
+        call_cpu("gca_count_cells", p_g, 1, self.nrows, self.ncols, self._empty, self._tree, self._fire, p_c, None)
+        return c
+
     def _award(self):
         """helicopter.py:120-135."""
         ncells = self.nrows * self.ncols
-        dict_counts = self.count_cells(self.grid)
-        cell_counts = np.array([dict_counts[self._empty], dict_counts[self._tree], dict_counts[self._fire]])
+        if _backend.choose(self.backend, dev.is_device_tensor(self.grid), ncells) == "cpu":
+            cell_counts = self._host_counts(self.grid)  # the same three counts, without the Counter round trip
+        else:
+            dict_counts = self.count_cells(self.grid)
+            cell_counts = np.array([dict_counts[self._empty], dict_counts[self._tree], dict_counts[self._fire]])
         cell_counts_relative = cell_counts / ncells
         reward_weights = np.array([self._reward_per_empty, self._reward_per_tree, self._reward_per_fire])
         return np.dot(reward_weights, cell_counts_relative)

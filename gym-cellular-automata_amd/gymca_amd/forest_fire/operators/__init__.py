@@ -3,10 +3,9 @@ from .ca_alexandridis import PartiallyObservableForestFire, PartiallyObservableF
 from .ca_DrosselSchwabl import ForestFire
 from .ca_windy import WindyForestFire
 from .move_modify import Modify, Move, MoveModify
+from .move_modify_jax import ModifyJax, MoveJax, MoveModifyJax
 from .repeat_ca import RepeatCA
-
-# The JAX-suffixed operators of the reference are served by the same classes.
-MoveJax, ModifyJax, MoveModifyJax, RepeatCAJax = Move, Modify, MoveModify, RepeatCA
+from .repeat_ca_jax import RepeatCAJax
 
 __all__ = ["WindyForestFire", "PartiallyObservableForestFire", "PartiallyObservableForestFireJax", "ForestFire",
            "Move", "Modify", "MoveModify", "RepeatCA", "MoveJax", "ModifyJax", "MoveModifyJax", "RepeatCAJax"]

@@ -123,9 +123,15 @@ class PartiallyObservableForestFireJax(Operator):
 
     deterministic = False
 
-    def __init__(self, grid_size, empty, tree, fire, *args, pinecones=False, **kwargs):
+    def __init__(self, grid_size, empty, tree, fire, *args, pinecones=False, env_offset=0, key_is_step=False,
+                 **kwargs):
         super().__init__(*args, **kwargs)
         self.grid_size = grid_size
+        # env_offset: global id of env 0 of a stack (Philox counters carry it, like the batched env's shards);
+        # key_is_step: per_env_context["key"] holds the per-env Philox step counter (the Advanced env's context
+        # layout, where the operator's own philox_seed is the env's key) instead of a Philox seed
+        self.env_offset = int(env_offset)
+        self.key_is_step = bool(key_is_step)
         # pinecone spotting (:229-319, :400-420): commented out in the reference; gca_alex_pinecones here
         self.pinecones = bool(pinecones)
         c = alex_constants(grid_size)
@@ -170,12 +176,20 @@ class PartiallyObservableForestFireJax(Operator):
         dous = u8(ctx.get("dousing_count", np.zeros((E, H, W))), (E, H, W))
         slope = d(ctx["slope"], torch.float32, (E, H, W, 9))
         p_slope = torch.empty((E, 8, H, W), dtype=torch.float32, device=device)
-        widx = d(np.asarray(ctx["wind_index"]).reshape(E), torch.int32, (E,))
-        rng_step = d(np.asarray(ctx.get("rng_step", 0), dtype=np.int64).reshape(-1).astype(np.uint32).view(np.int32)
-                     * np.ones(E, dtype=np.int32), torch.int32, (E,))
-        seed = key_to_seed(ctx.get("key", self.philox_seed))
+        wi_src = ctx["wind_index"]
+        widx = d(wi_src if dev.is_device_tensor(wi_src) else np.asarray(wi_src).reshape(E), torch.int32, (E,))
+        if self.key_is_step:
+            k = ctx["key"]
+            rng_step = (k.to(device=device, dtype=torch.int32).reshape(E).contiguous() if dev.is_device_tensor(k)
+                        else d(np.asarray(k, dtype=np.int64).reshape(-1).astype(np.uint32).view(np.int32)
+                               * np.ones(E, dtype=np.int32), torch.int32, (E,)))
+            seed = self.philox_seed
+        else:
+            rng_step = d(np.asarray(ctx.get("rng_step", 0), dtype=np.int64).reshape(-1).astype(np.uint32)
+                         .view(np.int32) * np.ones(E, dtype=np.int32), torch.int32, (E,))
+            seed = key_to_seed(ctx.get("key", self.philox_seed))
         p, _ = make_alex_params(self.grid_size, self.empty, self.tree, self.fire, shared_context["winds"],
-                                shared_context.get("p_tree", 0.0), seed)
+                                shared_context.get("p_tree", 0.0), seed, self.env_offset)
         st = dev.stream_ptr(device)
         call("gca_alex_prepare_slope", dev.ptr(slope), dev.ptr(p_slope), E, H, W, st)
         grid_out = torch.empty_like(grid_in)
@@ -195,25 +209,30 @@ class PartiallyObservableForestFireJax(Operator):
         if self.pinecones:  # on the step's output, with the wind of the step (before its change)
             from .pinecones import make_pine_params, s_cdf_tables
 
-            pp = make_pine_params(seed, self.empty, self.tree, self.fire)
+            pp = make_pine_params(seed, self.empty, self.tree, self.fire, self.env_offset)
             tabs = torch.as_tensor(s_cdf_tables(shared_context["winds"]).view(np.int32), device=device)
             call("gca_alex_pinecones", pp, E, H, W, dev.ptr(grid_in), dev.ptr(grid_out), dev.ptr(age_out),
                  dev.ptr(veg), dev.ptr(den), dev.ptr(widx), dev.ptr(tabs), dev.ptr(rng_step), None, None, st)
         new_widx = widx.clone()
         call("gca_alex_wind_change", float(np.float32(shared_context.get("p_wind_change", 0.06))), p.n_winds,
-             p.seed, 0, dev.ptr(rng_step), dev.ptr(wu), dev.ptr(wk), dev.ptr(new_widx), E, st)
+             p.seed, self.env_offset, dev.ptr(rng_step), dev.ptr(wu), dev.ptr(wk), dev.ptr(new_widx), E, st)
 
         out_ctx = dict(ctx)
         if dev.is_device_tensor(grid):
             new_grid = grid_out.reshape(shape)
             out_ctx["fire_age"] = age_out.reshape(shape)
-            out_ctx["wind_index"] = new_widx if E > 1 else new_widx[0]
+            out_ctx["wind_index"] = new_widx.reshape(tuple(wi_src.shape)) if dev.is_device_tensor(wi_src) else \
+                (new_widx if E > 1 else new_widx[0])
         else:
             new_grid = grid_out.cpu().numpy().reshape(shape).astype(np.asarray(grid).dtype)
             out_ctx["fire_age"] = age_out.cpu().numpy().reshape(shape).astype(np.float32)
             wi = new_widx.cpu().numpy()
-            out_ctx["wind_index"] = wi if E > 1 else np.int32(wi[0])
-        out_ctx["rng_step"] = int(np.asarray(ctx.get("rng_step", 0)).reshape(-1)[0]) + 1
+            out_ctx["wind_index"] = wi.reshape(np.shape(wi_src)) if np.ndim(wi_src) else np.int32(wi[0])
+        if self.key_is_step:  # the step counter advances like the env's (gca_advenv_post: rng_step += 1)
+            k = ctx["key"]
+            out_ctx["key"] = k + 1 if dev.is_device_tensor(k) else np.asarray(k) + 1
+        else:
+            out_ctx["rng_step"] = int(np.asarray(ctx.get("rng_step", 0)).reshape(-1)[0]) + 1
         if return_probs:
             return new_grid, out_ctx, shared_context, probs.cpu().numpy().reshape(shape + (8,))
         return new_grid, out_ctx, shared_context

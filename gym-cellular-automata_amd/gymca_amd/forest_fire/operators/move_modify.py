@@ -1,14 +1,16 @@
 """Move / Modify / MoveModify — drop-ins for the reference operators (move_modify.py:10-134).
 
-The arithmetic runs in the device kernel gca_move_modify (one lane per env), so the
-same code path serves the single-env drop-in here and the batched envs. Semantics:
+The arithmetic is gca_move_modify (include/gca.h): the device kernel (one lane per env) for device tensors, the
+host build of the same symbol (libgca_cpu.so) for host arrays — the work is O(1) per env, so a device round
+trip would cost far more than the call (backend="hip" forces the kernel, see gymca_amd/_backend.py). Semantics:
 Move applies the four direction sets in order with bounds checks (:37-67); Modify
 substitutes `effects[grid[row, col]]` IN PLACE and sets `self.hit` (:84-94).
 """
 import numpy as np
 
+from ... import _backend
 from ... import _device as dev
-from ..._lib import BulldozerParams, call
+from ..._lib import BulldozerParams, call, call_cpu
 from ...operator import Operator
 from ...spaces import Tuple
 
@@ -41,12 +43,59 @@ def make_params(directions_sets=None, effects=None):
     return p
 
 
-def _run(params, grid, action_pair, position, with_grid):
-    """One env through gca_move_modify. Returns (new_position, hit, grid_out)."""
+_SCRATCH = _backend.Scratch()
+
+
+def _run_host(params, grid, action_pair, position, with_grid):
+    """One env through the host build of gca_move_modify (O(1): only the target cell is touched); the grid is
+    modified in place."""
+    arr = grid if isinstance(grid, np.ndarray) else np.asarray(grid)
+    H, W = arr.shape[-2:]
+    act, p_act = _SCRATCH.get("act", (1, 2), np.int32)
+    pos, p_pos = _SCRATCH.get("pos", (1, 2), np.int32)
+    hit, p_hit = _SCRATCH.get("hit", (1,), np.uint8)
+    act[0, 0], act[0, 1] = int(action_pair[0]), int(bool(action_pair[1]))
+    pos[0, 0], pos[0, 1] = int(position[0]), int(position[1])
+    hit[0] = 0
+    if with_grid and arr is grid and arr.dtype == np.uint8 and arr.flags["C_CONTIGUOUS"]:
+        call_cpu("gca_move_modify", params, p_act, p_pos, arr.ctypes.data, H, W, p_hit, 1, None)
+        return pos[0].astype(np.int64), bool(hit[0])
+    if with_grid and arr.ndim == 2 and H * W <= _backend.HOST_MAX_CELLS:  # small grid: one call on a u8 copy
+        g8, p_g8 = _SCRATCH.get("grid", (H, W), np.uint8)
+        if arr.size and (arr.min() < 0 or arr.max() > 255):
+            raise ValueError("cell values must fit the u8 layout (0..255)")
+        np.copyto(g8, arr, casting="unsafe")
+        call_cpu("gca_move_modify", params, p_act, p_pos, p_g8, H, W, p_hit, 1, None)
+        if hit[0]:
+            r, c = int(pos[0, 0]), int(pos[0, 1])
+            grid[r, c] = g8[r, c]
+        return pos[0].astype(np.int64), bool(hit[0])
+    call_cpu("gca_move_modify", params, p_act, p_pos, None, H, W, None, 1, None)  # Move
+    if with_grid:  # Modify of the one cell under the new position (move_modify.py:84-94), written back in place
+        r, c = int(pos[0, 0]), int(pos[0, 1])
+        v = int(arr[r, c])
+        if not 0 <= v <= 255:
+            raise ValueError("cell values must fit the u8 layout (0..255)")
+        cell, p_cell = _SCRATCH.get("cell", (1, 1), np.uint8)
+        act1, p_act1 = _SCRATCH.get("act1", (1, 2), np.int32)
+        pos1, p_pos1 = _SCRATCH.get("pos1", (1, 2), np.int32)
+        cell[0, 0] = v
+        act1[0, 0], act1[0, 1] = 31, 1  # 31: no movement bit set
+        pos1[0, 0] = pos1[0, 1] = 0
+        call_cpu("gca_move_modify", params, p_act1, p_pos1, p_cell, 1, 1, p_hit, 1, None)
+        if hit[0]:
+            grid[r, c] = cell[0, 0]
+    return pos[0].astype(np.int64), bool(hit[0])
+
+
+def _run(params, grid, action_pair, position, with_grid, backend=None):
+    """One env through gca_move_modify. Returns (new_position, hit); the grid is modified in place."""
     import torch
 
-    device = dev.require_device()
     on_device = dev.is_device_tensor(grid)
+    if _backend.choose(backend, on_device, 0, o1=True) == "cpu":
+        return _run_host(params, grid, action_pair, position, with_grid)
+    device = dev.require_device()
     shape = tuple(grid.shape)
     H, W = shape[-2:]
     act = torch.tensor([[int(action_pair[0]), int(bool(action_pair[1]))]], dtype=torch.int32, device=device)
@@ -79,8 +128,9 @@ class Move(Operator):
 
     deterministic = True
 
-    def __init__(self, directions_sets, *args, **kwargs):
+    def __init__(self, directions_sets, *args, backend=None, **kwargs):
         super().__init__(*args, **kwargs)
+        self.backend = backend
         self.up_set = directions_sets["up"]
         self.down_set = directions_sets["down"]
         self.left_set = directions_sets["left"]
@@ -90,7 +140,7 @@ class Move(Operator):
         self._params = make_params(directions_sets)
 
     def update(self, grid, action, context):
-        new_pos, _ = _run(self._params, grid, (int(action), 0), context, with_grid=False)
+        new_pos, _ = _run(self._params, grid, (int(action), 0), context, with_grid=False, backend=self.backend)
         return grid, new_pos
 
 
@@ -103,15 +153,17 @@ class Modify(Operator):
 
     deterministic = True
 
-    def __init__(self, effects, *args, **kwargs):
+    def __init__(self, effects, *args, backend=None, **kwargs):
         super().__init__(*args, **kwargs)
+        self.backend = backend
         self.effects = effects
         self._params = make_params(None, effects)
 
     def update(self, grid, action, context):
         self.hit = False
         if action:
-            _, self.hit = _run(self._params, grid, (31, 1), context, with_grid=True)  # 31: no movement bit set
+            _, self.hit = _run(self._params, grid, (31, 1), context, with_grid=True,  # 31: no movement bit set
+                               backend=self.backend)
         return grid, context
 
 
@@ -146,7 +198,9 @@ class MoveModify(Operator):
                      "right": self.move.right_set}
                 self._fused = make_params(d, self.modify.effects)
             shoot = bool(modify_action)
-            position, hit = _run(self._fused, grid, (int(move_action), int(shoot)), position, with_grid=shoot)
+            backend = self.move.backend if self.move.backend == self.modify.backend else None
+            position, hit = _run(self._fused, grid, (int(move_action), int(shoot)), position, with_grid=shoot,
+                                 backend=backend)
             self.modify.hit = hit
             return grid, position
         grid, position = self.move(grid, move_action, position)

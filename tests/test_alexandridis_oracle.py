@@ -29,7 +29,8 @@ def test_constants_match_reference_constructor(H):
                        rtol=1e-6, atol=0)
 
 
-@pytest.mark.parametrize("E,H,W,seed", [(2, 16, 16, 1), (1, 37, 45, 2), (2, 64, 64, 3), (1, 8, 8, 4)])
+@pytest.mark.parametrize("E,H,W,seed", [(2, 16, 16, 1), (1, 37, 45, 2), (2, 64, 64, 3), (1, 8, 8, 4),
+                                        (2, 256, 256, 5), (2, 512, 512, 6)])  # BASELINE sizes: R = 6 and 7
 def test_c_oracle_injected_matches_reference_restatement(E, H, W, seed):
     case = make_case(E, H, W, seed, p_tree=0.3)
     p = params(H, case["p_tree"])
@@ -55,8 +56,9 @@ def test_c_oracle_injected_matches_reference_restatement(E, H, W, seed):
         assert tuple(counts[e]) == tuple(int(np.sum(go[e] == v)) for v in (0, 1, 2))
 
 
-def test_probabilities_within_1e6_of_float64():
-    E, H, W = 2, 64, 64
+@pytest.mark.parametrize("H", [64, 256, 512])  # 256 / 512: BASELINE sizes (R = 6 / 7)
+def test_probabilities_within_1e6_of_float64(H):
+    E, W = 2, H
     case = make_case(E, H, W, 11)
     p = params(H, 0.0)
     ps = alex_c.prepare_slope(case["slope"])

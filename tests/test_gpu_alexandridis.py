@@ -125,6 +125,83 @@ def test_injected_mode_matches_reference_rule(device):
         assert np.array_equal(ao[e][~diff], na.astype(np.int16)[~diff])
 
 
+def _ref_compare(case, e, go, ao, po, slope9, p_tree, C):
+    """One env of a device step (injected draws) against the numpy restatement of the reference rule
+    (ca_alexandridis_jax.py:321-424) and the independent float64 probability: probabilities within
+    1e-6 (TOL), integer states equal except where a uniform lies within 1e-6 of its probability."""
+    H, W = case["grid"].shape[1:]
+    W8 = winds()[:, 0]
+    ub, ug, ua = case["draws"]
+    veg, den = case["veg"][e].astype(np.int64), case["den"][e].astype(np.int64)
+    ng, na, rp = ref.update_grid(case["grid"][e], case["age"][e], veg, den, slope9[e], case["dous"][e],
+                                 W8[case["widx"][e]], p_tree, ub[e], ug[e], ua[e], C)
+    sel = [0, 1, 2, 3, 5, 6, 7, 8]
+    rp8 = rp.reshape(H, W, 9)[..., sel]
+    assert np.max(np.abs(po[e] - rp8) / np.maximum(np.abs(rp8), 1.0)) < 1e-6  # TOL 1e-6 vs the f32 restatement
+    p64 = ref.burn_probability_f64(case["grid"][e], veg, den, W8[case["widx"][e]], slope9[e], case["dous"][e],
+                                   C).reshape(H, W, 9)[..., sel]
+    assert np.max(np.abs(po[e] - p64) / np.maximum(np.abs(p64), 1.0)) < 1e-6  # TOL 1e-6 vs float64
+    diff = go[e] != ng
+    if diff.any():
+        close = np.abs(ub[e].reshape(H, W, 9)[..., sel] - rp8).min(axis=-1) < 1e-6
+        assert np.all(close[diff])
+    assert diff.sum() <= 8  # near-ties are rare: a systematic rule difference would show thousands
+    assert np.array_equal(ao[e][~diff], na.astype(np.int16)[~diff])
+    return int((go[e] != case["grid"][e]).sum())
+
+
+@pytest.mark.parametrize("N,seed", [(256, 71), (512, 72)])
+def test_headline_sizes_injected_vs_reference_rule(device, N, seed):
+    """BASELINE sizes, deterministically: N = 256 (configs 3/4: heat radius R = 6, 13x13 window) and N = 512
+    (config 5's grid: R = 7, 15x15). Hidden-layer slopes from an altitude field (get_slope on the device),
+    vegetation / density 0..6 (the clip), dousing, p_tree > 0, E = 2, the reference's own draws injected.
+    1. gca_alex_step (8 p_slope planes) and gca_alex_step_es (edge slopes) vs the numpy restatement of
+       _update_grid (ca_alexandridis_jax.py:62,108-153,345-349,379-398) and the float64 probability;
+    2. the two layouts bit-identical (states, ages, counts, probabilities);
+    3. the headline kernel, gca_alex_step_packed (Philox mode, packed layout), bit-identical to
+       gca_alex_step_es in Philox mode on the same state, whose probabilities are bit-identical to the
+       injected-mode probabilities checked in 1 — so the timed kernel evaluates the reference's p_d."""
+    import torch
+
+    from gymca_amd import _device as dev
+    from gymca_amd._lib import call
+    from test_gpu_edge_slope import altitude, packed_step, slopes, step
+
+    E, p_tree = 2, 0.2
+    case = make_case(E, N, N, seed, p_tree=p_tree)
+    C = case["C"]
+    assert C["R"] == (6 if N == 256 else 7)
+    p = params(N, p_tree)
+    alt = altitude(E, N, N, seed)
+    es, ps = slopes(device, alt)
+    a = torch.as_tensor(alt, device=device)
+    s9 = torch.empty((E, N, N, 3, 3), dtype=torch.float32, device=device)
+    tmp = torch.empty((E, 8, N, N), dtype=torch.float32, device=device)
+    call("gca_alex_slope_from_altitude", dev.ptr(a), dev.ptr(tmp), dev.ptr(s9), E, N, N, dev.stream_ptr())
+    s9 = s9.cpu().numpy()
+    from gymca_amd.forest_fire.bulldozer.init_utils import get_slope
+
+    assert np.allclose(s9, get_slope(alt, N, N, E).astype(np.float32), rtol=3e-6, atol=1e-5)
+    case["slope"] = s9
+    inj = case["draws"]
+    r_planes = step(device, "gca_alex_step", p, case, ps, inj=inj, probs=True)
+    r_edge = step(device, "gca_alex_step_es", p, case, es, inj=inj, probs=True)
+    for x, y in zip(r_planes, r_edge):
+        assert np.array_equal(np.asarray(x).view(np.uint8), np.asarray(y).view(np.uint8))
+    go, ao, cnt, po = r_edge
+    changed = [_ref_compare(case, e, go, ao, po, s9, p_tree, C) for e in range(E)]
+    assert min(changed) > 1000  # the step did real work (ignitions, burn-outs, growth)
+    assert np.array_equal(cnt, np.stack([(go == v).sum(axis=(1, 2)) for v in (0, 1, 2)], axis=1))
+    # the chain to the timed kernel (Philox mode)
+    rs = np.full(E, 9, np.uint32)
+    case_ph = dict(case, dous=(case["dous"] > 0).astype(np.uint8))  # the packed layout's dousing bits
+    g_es, a_es, c_es, po_es = step(device, "gca_alex_step_es", p, case_ph, es, rng_step=rs, probs=True)
+    g_pk, a_pk, c_pk, _, _ = packed_step(device, p, case_ph, es, rs)
+    assert np.array_equal(g_pk, g_es) and np.array_equal(a_pk, a_es) and np.array_equal(c_pk, c_es)
+    _, _, _, po_inj = step(device, "gca_alex_step_es", p, case_ph, es, inj=inj, probs=True)
+    assert np.array_equal(po_es.view(np.uint32), po_inj.view(np.uint32))
+
+
 def test_dropin_operator_with_reference_draws(device):
     from gymca_amd.forest_fire.operators import PartiallyObservableForestFireJax
 

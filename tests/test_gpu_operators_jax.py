@@ -1,0 +1,191 @@
+"""GPU: the JAX-contract operators on device tensors (move_modify_jax.py:39-157, repeat_ca_jax.py:34-71), the
+Advanced env's per-env MDP (advanced_bulldozer.py:1103-1133) against the env's own step, and stateless_step's
+adoption of foreign context values (slope, shared p_tree / winds) against the oracle."""
+import numpy as np
+import pytest
+
+from alex_cases import make_case, winds
+from oracle import alex_c
+
+pytestmark = pytest.mark.gpu
+
+SETS = {"up": {0, 1, 2}, "down": {6, 7, 8}, "left": {0, 3, 6}, "right": {2, 5, 8}, "not_move": {4}}
+
+
+def test_move_modify_jax_on_device_matches_host(device):
+    import torch
+
+    from gymca_amd.forest_fire.operators import MoveJax, MoveModifyJax, ModifyJax
+
+    rng = np.random.default_rng(5)
+    E, H, W = 64, 11, 13
+    pos = np.stack([rng.integers(0, H, E), rng.integers(0, W, E)], axis=1)
+    moves, shots = rng.integers(0, 9, E), rng.integers(0, 2, E)
+    d0 = (rng.random((E, H, W)) < 0.1).astype(np.uint8)
+    host = MoveModifyJax(MoveJax(SETS, backend="cpu"), ModifyJax({}, backend="cpu"))
+    gpu = MoveModifyJax(MoveJax(SETS, backend="hip"), ModifyJax({}, backend="hip"))
+    _, hp, hpe = host(np.zeros((E, H, W)), (moves, shots), pos, {"dousing_count": d0.copy()})
+    dd = torch.as_tensor(d0, device=device)
+    _, gp, gpe = gpu(torch.zeros((E, H, W), device=device), (torch.as_tensor(moves, device=device),
+                     torch.as_tensor(shots, device=device)), torch.as_tensor(pos, device=device, dtype=torch.int32),
+                     {"dousing_count": dd})
+    assert np.array_equal(gp.cpu().numpy(), hp)
+    assert np.array_equal(gpe["dousing_count"].cpu().numpy(), hpe["dousing_count"])
+    assert np.array_equal(dd.cpu().numpy(), d0)  # functional: the caller's tensor is untouched
+
+
+def _op_ctx(case, e=None):
+    sl = slice(None) if e is None else e
+    return {"wind_index": case["widx"][sl], "density": case["den"][sl].astype(np.int64),
+            "vegetation": case["veg"][sl].astype(np.int64), "slope": case["slope"][sl],
+            "fire_age": case["age"][sl].astype(np.float32), "dousing_count": case["dous"][sl].astype(np.int32),
+            "key": np.array([3, 4], np.uint32), "rng_step": 5}
+
+
+@pytest.mark.parametrize("accu", [0.0, 0.95, 2.5])
+def test_repeat_ca_jax_one_device_step(device, accu):
+    """RepeatCAJax around PartiallyObservableForestFireJax: exactly one CA step (the kernel, Philox draws of the
+    context's key / rng_step) whatever the accumulated time, and the fraction carried."""
+    from gymca_amd.forest_fire.operators import PartiallyObservableForestFireJax, RepeatCAJax
+
+    N = 64
+    case = make_case(1, N, N, 8, p_tree=0.0)
+    ca = PartiallyObservableForestFireJax(N, 0, 1, 2)
+    shared = {"winds": winds(), "p_tree": np.float32(0.0), "p_wind_change": np.float32(0.06)}
+    grid = case["grid"][0].astype(np.float32)
+    want_grid, want_ctx, _ = ca(grid, None, _op_ctx(case, 0), shared)
+    op = RepeatCAJax(ca, lambda a: np.float32(0.7), lambda s: np.float32(0.001))
+    got_grid, (got_ctx, frac) = op(grid, (1, 0), _op_ctx(case, 0), shared, np.float32(accu))
+    assert np.array_equal(got_grid, want_grid) and np.array_equal(got_ctx["fire_age"], want_ctx["fire_age"])
+    assert got_ctx["rng_step"] == 6  # one step's draws consumed
+    exp, _ = np.modf(np.float32(accu) + (np.float32(0.7) + np.float32(0.001)))
+    assert frac == exp
+    eg, ea, _, _ = alex_c.alex_step(alex_c.params_from(_params(N, ca, case)), case["grid"], case["age"], case["veg"],
+                                    case["den"], case["dous"], alex_c.prepare_slope(case["slope"]), case["widx"],
+                                    rng_step=np.array([5], np.uint32))
+    assert np.array_equal(got_grid, eg[0]) and np.array_equal(got_ctx["fire_age"], ea[0].astype(np.float32))
+
+
+def _params(N, ca, case):
+    from gymca_amd.forest_fire.operators.ca_alexandridis import key_to_seed, make_alex_params
+
+    p, _ = make_alex_params(N, 0, 1, 2, winds(), 0.0, key_to_seed(np.array([3, 4], np.uint32)))
+    return p
+
+
+def _full_actions(rng, E):
+    """(E, 3) (move, shoot, extension choice) and the _create_full_actions form (move, shoot, binary flags)."""
+    from gymca_amd.forest_fire.bulldozer.observation import EXTENSION_LOOKUP
+
+    a3 = np.stack([rng.integers(0, 9, E), rng.integers(0, 2, E), rng.integers(0, len(EXTENSION_LOOKUP), E)], axis=1)
+    full = np.concatenate([a3[:, :2], EXTENSION_LOOKUP[a3[:, 2]]], axis=1)
+    return a3, full
+
+
+@pytest.mark.parametrize("E,N,enable_ext", [(3, 64, False), (2, 48, True), (1, 32, False)])
+def test_env_mdp_update_reproduces_env_step(device, E, N, enable_ext):
+    """env.MDP.update(grid, action, per_env_context, shared_context, position, time) — the reference's per-env
+    MDP, here on the vmapped (E, ...) arguments in the reference's context layout (reference_context()) —
+    reproduces env.step bit for bit: grid, fire ages, wind index, step key, dousing, position, time, time_step,
+    is_night and the RGB observation."""
+    import torch
+
+    from gymca_amd.forest_fire.bulldozer import AdvancedForestFireBulldozerEnv
+
+    env = AdvancedForestFireBulldozerEnv(N, N, key=17, num_envs=E, use_hidden=True, device=device,
+                                         hidden_rng=np.random.RandomState(2), enable_extensions=enable_ext)
+    env.reset()
+    case = make_case(E, N, N, 40)
+    env.set_state(grid=case["grid"], fire_age=case["age"], wind_index=case["widx"])
+    env.is_night.fill_(1)
+    env.time_step.fill_(398)  # crosses the day_length = 400 toggle
+    mdp = env.MDP
+    rng = np.random.default_rng(1)
+    for t in range(5):
+        ctx = env.reference_context()
+        pe, shared = ctx["per_env_context"], ctx["shared_context"]
+        a3, full = _full_actions(rng, E)
+        (rgb, g, ext), (npe, npos, ntime) = mdp.update(pe["true_grid"], torch.as_tensor(full, device=device), pe,
+                                                       shared, ctx["position"], ctx["time"])
+        env.step(a3)
+        st = f"step {t}"
+        assert torch.equal(g.to(torch.uint8), env.grid[env.cur]), st
+        assert torch.equal(npe["true_grid"].to(torch.uint8), env.grid[env.cur])
+        assert torch.equal(npe["fire_age"].to(torch.int16), env.age[env.cur]), st
+        assert torch.equal(npe["wind_index"].to(torch.int32), env.wind_index), st
+        assert torch.equal(npe["key"].to(torch.int32), env.rng_step), st
+        assert torch.equal(npe["dousing_count"].to(torch.uint8), env.dousing), st
+        assert torch.equal(npos.to(torch.int32), env.pos) and torch.equal(ntime, env.accu), st
+        assert torch.equal(npe["time_step"], env.time_step) and torch.equal(npe["is_night"], env.is_night), st
+        assert torch.equal(rgb, env.rgb), st
+        assert ext.shape == (E, N, N, 5)
+
+
+def test_stateless_step_honours_foreign_p_tree_and_winds(device):
+    """A shared_context with another p_tree and wind table changes the step exactly as the oracle predicts
+    (ca_alexandridis_jax.py:386, :428)."""
+    from gymca_amd.forest_fire.bulldozer import AdvancedForestFireBulldozerEnv
+    from gymca_amd.forest_fire.operators.ca_alexandridis import make_alex_params
+
+    E, N = 2, 64
+    env = AdvancedForestFireBulldozerEnv(N, N, key=9, num_envs=E, use_hidden=True, device=device,
+                                         hidden_rng=np.random.RandomState(1), observation="grid")
+    obs, info = env.reset()
+    case = make_case(E, N, N, 12)
+    env.set_state(grid=case["grid"], fire_age=case["age"], wind_index=case["widx"])
+    g0, a0 = case["grid"].copy(), case["age"].copy()
+    ps = env.p_slope_planes().cpu().numpy()
+    veg, den = env.vegetation.cpu().numpy(), env.density.cpu().numpy()
+    w2 = winds()[::-1].copy()  # another table: the same matrices in reverse order
+    obs[1]["shared_context"] = dict(obs[1]["shared_context"], p_tree=0.4, winds=w2)
+    env.stateless_step(np.zeros((E, 3), np.int64), obs, info)
+    p, _ = make_alex_params(N, 0, 1, 2, w2, 0.4, env.key, env.env_offset)
+    eg, ea, _, _ = alex_c.alex_step(p, g0, a0, veg, den, np.zeros((E, N, N), np.uint8), ps, case["widx"],
+                                    rng_step=np.zeros(E, np.uint32))
+    assert np.array_equal(env.grid[env.cur].cpu().numpy(), eg) and np.array_equal(env.age[env.cur].cpu().numpy(), ea)
+    assert (eg[g0 == 0] == 1).any()  # p_tree = 0.4 grew trees: the foreign value was used
+
+
+def test_stateless_step_honours_foreign_reference_slope(device):
+    """A slope in the reference's (E, N, N, 3, 3) layout (not derivable from an altitude) switches the env to the
+    general 8-plane layout and the step follows it exactly (ca_alexandridis_jax.py:199-200)."""
+    from gymca_amd.forest_fire.bulldozer import AdvancedForestFireBulldozerEnv
+
+    E, N = 2, 256
+    env = AdvancedForestFireBulldozerEnv(N, N, key=4, num_envs=E, use_hidden=True, device=device,
+                                         hidden_rng=np.random.RandomState(3), observation="grid")
+    assert env.slope_layout == "packed"
+    obs, info = env.reset()
+    case = make_case(E, N, N, 13)
+    env.set_state(grid=case["grid"], fire_age=case["age"], wind_index=case["widx"])
+    veg, den = env.vegetation.cpu().numpy(), env.density.cpu().numpy()
+    obs[1]["per_env_context"]["slope"] = case["slope"]  # random, not antisymmetric
+    env.stateless_step(np.zeros((E, 3), np.int64), obs, info)
+    assert env.slope_layout == "planes"
+    eg, ea, _, _ = alex_c.alex_step(alex_c.params_from(env.alex_params), case["grid"], case["age"], veg, den,
+                                    np.zeros((E, N, N), np.uint8), alex_c.prepare_slope(case["slope"]), case["widx"],
+                                    rng_step=np.zeros(E, np.uint32))
+    assert np.array_equal(env.grid[env.cur].cpu().numpy(), eg) and np.array_equal(env.age[env.cur].cpu().numpy(), ea)
+    env.step(np.zeros((E, 2), np.int64))  # and keeps stepping on the new layout
+
+
+def test_stateless_step_refuses_before_writing(device):
+    """Invalid foreign values raise ValueError and leave the env's state as it was (validated before any copy)."""
+    from gymca_amd.forest_fire.bulldozer import AdvancedForestFireBulldozerEnv
+
+    E, N = 2, 256
+    env = AdvancedForestFireBulldozerEnv(N, N, key=4, num_envs=E, use_hidden=False, device=device, observation="grid")
+    obs, info = env.reset()
+    g0 = env.grid[env.cur].clone()
+    bad = [("dousing_count", np.full((E, N, N), 2, np.int32)),  # the packed layout keeps dousing as bits
+           ("true_grid", np.full((E, N, N), 1.5, np.float32)),
+           ("fire_age", np.full((E, N, N), 40000.0, np.float32)),
+           ("slope", np.zeros((E, N, 3, 3), np.float32))]
+    for key, val in bad:
+        pe = dict(obs[1]["per_env_context"])
+        pe["true_grid"] = np.zeros((E, N, N))  # a valid foreign value next to the invalid one: not written either
+        pe[key] = val
+        o = (obs[0], dict(obs[1], per_env_context=pe))
+        with pytest.raises(ValueError):
+            env.stateless_step(np.zeros((E, 3), np.int64), o, info)
+        assert bool((env.grid[env.cur] == g0).all()), key
