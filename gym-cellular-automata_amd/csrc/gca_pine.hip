@@ -293,14 +293,14 @@ extern "C" int gca_alex_pinecones_classic(const gca_pine_classic_params* p, int 
     hipStream_t st = (hipStream_t)stream;
     if (in_lds) {
         const size_t lds = (size_t)16 * NW;
-        static size_t lds_set = 0;  // raise the dynamic-LDS ceiling once per size class (host-side attribute)
-        if (lds > 65536 && lds > lds_set) {
-            if (hipFuncSetAttribute(reinterpret_cast<const void*>(&alex_pinecones_classic_kernel<true>),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
-                gca_set_error("alex_pinecones_classic: hipFuncSetAttribute(%zu B LDS) failed", lds);
-                return GCA_ERR_HIP;
-            }
-            lds_set = lds;
+        // raise the dynamic-LDS ceiling on every launch above 64 KiB: the attribute is per device (and cheap), so a
+        // process-wide "already set" cache would skip it on a second GPU. GCA_PINEC_LDS_MAX_HW = 512 * 512 keeps the
+        // bitmaps at <= 128 KiB, leaving room under the 160 KiB per-workgroup limit for the static LDS of
+        // __syncthreads_or's work-group reduction.
+        if (lds > 65536 && hipFuncSetAttribute(reinterpret_cast<const void*>(&alex_pinecones_classic_kernel<true>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
+            gca_set_error("alex_pinecones_classic: hipFuncSetAttribute(%zu B LDS) failed", lds);
+            return GCA_ERR_HIP;
         }
         hipLaunchKernelGGL(alex_pinecones_classic_kernel<true>, dim3(E), dim3(512), lds, st, *p, H, W, NW, grid_in,
                            grid_out, age_out, veg, den, wind_index, s_cdf, rng_step, counts, nullptr);

@@ -33,7 +33,7 @@ TAG_PINEC = 0x50434C00
 TAG_PINEC_AGE = 0x50434C41
 GCA_PINEC_NMAX = 16
 GCA_PINEC_CDF = 48
-GCA_PINEC_LDS_MAX_HW = 327680
+GCA_PINEC_LDS_MAX_HW = 262144
 
 
 class GCAError(RuntimeError):

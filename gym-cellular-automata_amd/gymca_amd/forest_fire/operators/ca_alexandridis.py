@@ -103,6 +103,8 @@ def make_alex_params(grid_size, empty, tree, fire, winds, p_tree, seed, env_offs
 
 def wind_matrices(winds):
     """shared_context['winds'] is (n, 2, 3, 3) = (wind_matrix, ft) pairs (:428); also accept (n, 3, 3)."""
+    if dev.is_device_tensor(winds):
+        winds = winds.cpu().numpy()
     w = np.asarray(winds, dtype=np.float32)
     if w.ndim == 4:
         w = w[:, 0]

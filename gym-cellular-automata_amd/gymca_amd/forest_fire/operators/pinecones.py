@@ -20,6 +20,8 @@ evaluated in float64 exactly as the reference writes it.
 """
 import math
 
+import functools
+
 import numpy as np
 
 from ..._lib import GCA_PINE_CDF, GCA_PINE_MAX, GCA_PINEC_CDF, GCA_PINEC_NMAX, PineClassicParams, PineParams
@@ -72,12 +74,25 @@ def thrust_law(f, K=None):
     return ks, hi - lo
 
 
-def s_cdf_tables(winds):
-    """(n_winds, 8, GCA_PINE_CDF) u32 from shared_context["winds"] (n, 2, 3, 3): the ft matrix of each wind
-    at ft_lookup[direction]."""
-    w = np.asarray(winds, dtype=np.float32)
+def _host_winds(winds):
+    if hasattr(winds, "is_cuda") and winds.is_cuda:
+        winds = winds.cpu().numpy()
+    w = np.ascontiguousarray(np.asarray(winds, dtype=np.float32))
     if w.ndim != 4 or w.shape[1] != 2:
         raise ValueError("winds must be (n, 2, 3, 3) (wind_matrix, ft) pairs")
+    return w
+
+
+def s_cdf_tables(winds):
+    """(n_winds, 8, GCA_PINE_CDF) u32 from shared_context["winds"] (n, 2, 3, 3): the ft matrix of each wind
+    at ft_lookup[direction]. Memoised on the table's contents (the operators call it per step)."""
+    w = _host_winds(winds)
+    return _s_cdf_tables(w.tobytes(), w.shape).copy()
+
+
+@functools.lru_cache(maxsize=16)
+def _s_cdf_tables(raw, shape):
+    w = np.frombuffer(raw, dtype=np.float32).reshape(shape)
     return np.stack([np.stack([thrust_table(w[i, 1][a, b]) for (a, b) in FT_LOOKUP]) for i in range(len(w))])
 
 
@@ -124,10 +139,15 @@ def classic_burn_thresholds():
 
 
 def classic_thrust_tables(winds):
-    """(n_winds, 8, GCA_PINEC_CDF) u32: thrust tables of f = 3 ft[lookup[d]] per (wind, direction)."""
-    w = np.asarray(winds, dtype=np.float32)
-    if w.ndim != 4 or w.shape[1] != 2:
-        raise ValueError("winds must be (n, 2, 3, 3) (wind_matrix, ft) pairs")
+    """(n_winds, 8, GCA_PINEC_CDF) u32: thrust tables of f = 3 ft[lookup[d]] per (wind, direction). Memoised on
+    the table's contents."""
+    w = _host_winds(winds)
+    return _classic_thrust_tables(w.tobytes(), w.shape).copy()
+
+
+@functools.lru_cache(maxsize=16)
+def _classic_thrust_tables(raw, shape):
+    w = np.frombuffer(raw, dtype=np.float32).reshape(shape)
     return np.stack([np.stack([thrust_table(CLASSIC_THRUST * float(w[i, 1][a, b]), GCA_PINEC_CDF, CLASSIC_THRUST)
                                for (a, b) in FT_LOOKUP]) for i in range(len(w))])
 

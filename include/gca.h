@@ -284,12 +284,12 @@ int gca_alex_pinecones(const gca_pine_params* p, int E, int H, int W, const uint
  * one count moves from the target's previous state to FIRE per ignited target.
  * s_cdf [n_winds][8][GCA_PINEC_CDF] u32: per (wind, direction) t[0] = 2K, t[1..2K] thresholds of
  * P(round(3 ft Z) <= -K + j) * 2^32. scratch: NULL when 16 * ceil(H W / 32) bytes fit one workgroup's LDS
- * (H W <= 327680, e.g. 512 x 512), else E * 4 * ceil(H W / 32) u32 of device memory (the kernel clears it).
+ * (H W <= 262144 = 512 x 512), else E * 4 * ceil(H W / 32) u32 of device memory (the kernel clears it).
  * Draws: Philox (lin, env, step, PINEC + 0) -> N, (lin, env, step, PINEC + 1 + m) -> s (word 0), u (word 1 >> 8),
  * d (word 2 >> 29); (target lin, env, step, PINEC_AGE) word 0 -> age. */
 #define GCA_PINEC_NMAX 16
 #define GCA_PINEC_CDF 48
-#define GCA_PINEC_LDS_MAX_HW 327680
+#define GCA_PINEC_LDS_MAX_HW 262144
 typedef struct {
     uint32_t n_cdf[GCA_PINEC_NMAX]; /* P(Poisson(1) <= j) * 2^32, j = 0..15 (N_p = poisson(), :37)              */
     int32_t dx[8], dy[8];           /* dx_lookup / dy_lookup (:63-64)                                          */

@@ -18,6 +18,15 @@ Fixture inventory:
   drossel.npz      ForestFire (Drossel-Schwabl)      ca_DrosselSchwabl.py:32-66
   helicopter.npz   ForestFireHelicopterEnv 5x5       helicopter.py:20-236
   moore.npz        moore_n                           neighbors.py:6-147
+  alexandridis_classic.npz
+                   PartiallyObservableForestFire.update   ca_alexandridis.py:35-221, 8-12 consecutive
+                   steps per case with pinecone spotting and skip-list events. The module's
+                   `import jax.numpy as np` (:1) gets numpy itself (it only calls exp / array /
+                   any / sum / np.random there; jax.numpy lacks np.random, :189, which is why the
+                   module cannot run as published). Every draw of op.np_random and of the global
+                   np.random.standard_normal is recorded in call order and attributed to the cell
+                   being visited, then stored as the array-form draws oracle/alexandridis_classic
+                   takes (burn, grow, age, wind; pinecone n / dirs / thrust / u / target age).
   init_utils.npz   init_vegetation / init_density / init_altitude / get_slope after
                    np.random.seed(k) (bulldozer/utils/init_utils.py:10-200). Those functions
                    use numpy and the global legacy np.random state only; the module's own
@@ -315,8 +324,173 @@ def gen_init_utils(R, rng):
     return out
 
 
+def _classic_context(rng, H, W, n_winds=8, fire_frac=0.2):
+    """Inputs of one classic case (the reference's context keys, ca_alexandridis.py:137-146)."""
+    import math
+
+    grid = rng.choice(np.array([0, 1, 2]), size=(H, W), p=[0.15, 0.85 - fire_frac, fire_frac])
+    winds = np.zeros((n_winds, 2, 3, 3))
+    for k in range(n_winds):  # calc_pw's (e^0.45 ft, ft) pairs (init_utils.py:225-244), 8 directions
+        th = k * 2 * math.pi / n_winds
+        for i in range(3):
+            for j in range(3):
+                if (i, j) != (1, 1):
+                    ft = math.exp(1.31 * (math.cos(math.atan2(1 - i, j - 1) - th) - 1))
+                    winds[k, :, i, j] = (math.exp(0.45) * ft, ft)
+    return {"winds": winds.astype(np.float32), "wind_index": int(rng.integers(0, n_winds)),
+            "density": rng.integers(1, 6, (H, W)), "vegetation": rng.integers(1, 6, (H, W)),
+            "slope": rng.uniform(-25, 25, (H, W, 3, 3)).astype(np.float32), "altitude": np.zeros((H, W)),
+            "p_tree": 0.1, "p_wind_change": 0.3,
+            "fire_age": np.where(grid == 2, rng.integers(1, 7, (H, W)), 0).astype(np.int64)}, grid
+
+
+class _Recorder:
+    """op.np_random stand-in: the seeded Generator's own draws, logged in call order with the visited cell."""
+
+    def __init__(self, gen, log, cur):
+        self.gen, self.log, self.cur = gen, log, cur
+
+    def _rec(self, kind, v, extra=None):
+        self.log.append((kind, self.cur[0], v, extra))
+        return v
+
+    def uniform(self, low=0.0, high=1.0, size=None):
+        return self._rec("uniform", self.gen.uniform(low, high, size), size)
+
+    def integers(self, low, high=None, size=None):
+        return self._rec("integers", self.gen.integers(low, high, size), (low, high))
+
+    def choice(self, a, size=None, replace=True, p=None):
+        return self._rec("choice", self.gen.choice(a, size=size, replace=replace, p=p), float(p[0]))
+
+    def poisson(self, lam=1.0, size=None):
+        return self._rec("poisson", self.gen.poisson(lam, size), None)
+
+
+def gen_alexandridis_classic(R, rng):
+    """The classic operator run as published with jax.numpy -> numpy, its draws recorded (see module doc)."""
+    import contextlib
+    import io
+
+    jax = types.ModuleType("jax")
+    jax.numpy = np
+    saved = {k: sys.modules.get(k) for k in ("jax", "jax.numpy")}
+    sys.modules.update({"jax": jax, "jax.numpy": np})
+    try:
+        cl = _load("gym_cellular_automata.forest_fire.operators.ca_alexandridis",
+                   f"{REF}/forest_fire/operators/ca_alexandridis.py")
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                sys.modules.pop(k, None)
+            else:
+                sys.modules[k] = v
+    DX, DY = [1, 1, 0, -1, -1, -1, 0, 1], [0, 1, 1, 1, 0, -1, -1, -1]  # :63-64
+    LOOKUP = [(0, 0), (0, 1), (0, 2), (1, 0), (1, 2), (2, 0), (2, 1), (2, 2)]  # :50-59
+    M = 16
+    out = {}
+    cases = [(16, 16, 8), (20, 24, 10), (32, 32, 12), (24, 17, 8)]
+    for ci, (H, W, steps) in enumerate(cases):
+        ctx, grid = _classic_context(rng, H, W)
+        out[f"c{ci}_winds"], out[f"c{ci}_density"] = ctx["winds"], ctx["density"]
+        out[f"c{ci}_vegetation"], out[f"c{ci}_slope"] = ctx["vegetation"], ctx["slope"]
+        out[f"c{ci}_p"] = np.array([ctx["p_tree"], ctx["p_wind_change"]])
+        op = cl.PartiallyObservableForestFire(0, 1, 2)
+        log, cur = [], [None]
+        op.np_random = _Recorder(np.random.default_rng(777 + ci), log, cur)
+        np.random.seed(555 + ci)  # the global legacy stream of :189
+        orig_nb, orig_sn = cl.neighborhood_at, np.random.standard_normal
+        orig_spf = op._set_fire_pinecone
+
+        def nb(grid_, pos, *a, **k):
+            cur[0] = tuple(int(v) for v in pos)
+            return orig_nb(grid_, pos, *a, **k)
+
+        def sn(n):
+            v = orig_sn(n)
+            log.append(("normal", cur[0], v, None))
+            return v
+
+        def spf(row, col, *a, **k):
+            log.append(("pine_target", cur[0], (int(row), int(col)), None))
+            return orig_spf(row, col, *a, **k)
+
+        cl.neighborhood_at, np.random.standard_normal, op._set_fire_pinecone = nb, sn, spf
+        try:
+            for t in range(steps):
+                log.clear()
+                g_in, a_in, w_in = grid.copy(), ctx["fire_age"].copy(), int(ctx["wind_index"])
+                with contextlib.redirect_stdout(io.StringIO()):  # :220 prints the wind change
+                    grid, ctx = op.update(grid, None, ctx)
+                ft = ctx["winds"][w_in][1]
+                burn, grow = np.ones((H, W, 3, 3)), np.ones((H, W))
+                age, pine_age = np.full((H, W), 4), np.full((H, W), 4)
+                n, dirs = np.zeros((H, W), np.int64), np.zeros((H, W, M), np.int64)
+                thrust, u = np.zeros((H, W, M)), np.ones((H, W, M))
+                wind_u, wind_k = 1.0, 1
+                pine_hits = np.zeros((H, W), np.uint8)
+                valid, k_valid, last = {}, {}, None
+                for kind, cell, v, extra in log:
+                    if kind == "uniform" and extra == (3, 3):  # _set_fire's burn draws (:104)
+                        burn[cell] = v
+                        last = ("fire", cell)
+                    elif kind == "uniform":  # _set_fire_pinecone's draw (:127) for the source's next valid landing
+                        i = valid[cell][k_valid[cell]]
+                        k_valid[cell] += 1
+                        u[cell + (i,)] = v
+                        last = ("pine", target)
+                    elif kind == "pine_target":
+                        target = v
+                    elif kind == "integers" and extra == (4, 11):
+                        if last[0] == "fire":
+                            age[last[1]] = v
+                        else:
+                            pine_age[last[1]] = v  # the last ignition of a target sets its age
+                            pine_hits[last[1]] = 1
+                    elif kind == "integers" and extra == (0, 8):  # pinecone directions (:47)
+                        nn = len(v)
+                        assert nn <= M
+                        dirs[cell + (slice(0, nn),)] = v
+                    elif kind == "poisson":
+                        n[cell] = v
+                        valid[cell], k_valid[cell] = [], 0
+                    elif kind == "normal":  # thrust of :189-190 and the landings it gives (:191-200)
+                        d = dirs[cell][:n[cell]]
+                        gi = np.array([LOOKUP[x] for x in d])
+                        th = 3 * v
+                        th = th * ft[tuple(zip(*gi))]
+                        thrust[cell + (slice(0, len(th)),)] = th
+                        r, c = cell
+                        for i in range(len(th)):
+                            nr, nc = round(r + DX[d[i]] * th[i]), round(c + DY[d[i]] * th[i])
+                            if 0 <= nr < H and 0 <= nc < W and (nr, nc) != (r, c):
+                                valid[cell].append(i)
+                    elif kind == "choice" and extra == ctx["p_tree"]:  # growth (:173-175)
+                        grow[cell] = 0.0 if v else 1.0
+                    elif kind == "choice":  # wind change (:212-214)
+                        wind_u = 0.0 if v else 1.0
+                    elif kind == "integers" and extra == (1, 8):
+                        wind_k = int(v)
+                    else:
+                        raise AssertionError(f"unexpected draw {kind} {extra}")
+                pre = f"c{ci}_s{t}_"
+                out.update({pre + "grid": g_in.astype(np.uint8), pre + "age": a_in, pre + "wind": np.array(w_in),
+                            pre + "burn": burn, pre + "grow": grow, pre + "draw_age": age,
+                            pre + "wind_u": np.array(wind_u), pre + "wind_k": np.array(wind_k),
+                            pre + "pine_n": n, pre + "pine_dirs": dirs, pre + "pine_thrust": thrust, pre + "pine_u": u,
+                            pre + "pine_age": pine_age, pre + "pine_hits": pine_hits,
+                            pre + "out_grid": np.asarray(grid).astype(np.uint8), pre + "out_age": ctx["fire_age"].copy(),
+                            pre + "out_wind": np.array(int(ctx["wind_index"]))})
+        finally:
+            cl.neighborhood_at, np.random.standard_normal = orig_nb, orig_sn
+        out[f"c{ci}_steps"] = np.array(steps)
+    out["n"] = np.array(len(cases))
+    return out
+
+
 GENERATORS = {"windy": gen_windy, "repeat_ca": gen_repeat, "move_modify": gen_move_modify, "bulldozer": gen_bulldozer,
-              "drossel": gen_drossel, "helicopter": gen_helicopter, "moore": gen_moore, "init_utils": gen_init_utils}
+              "drossel": gen_drossel, "helicopter": gen_helicopter, "moore": gen_moore, "init_utils": gen_init_utils,
+              "alexandridis_classic": gen_alexandridis_classic}
 
 
 def main():

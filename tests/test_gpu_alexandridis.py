@@ -487,3 +487,32 @@ def test_packed_fast_kernel_burn_law_chi_square(device):
     var = T * np.bincount(b, weights=laws * (1 - laws), minlength=B)
     stat = float(((o - ex) ** 2 / var).sum())
     assert stat < chi2.isf(1e-6, B), (stat, chi2.isf(1e-6, B))
+
+
+def test_classic_dropin_vs_reference_run(device, golden):
+    """The device drop-in PartiallyObservableForestFire (classic params on gca_alex_step, the reference's recorded
+    draws injected) against the reference's own update loop (tests/golden/alexandridis_classic.npz, 38 steps):
+    every cell no pinecone ignited (the fixture marks them; pinecones draw from Philox on the device and are
+    pinned through the oracle: oracle == reference run on this fixture, device == oracle on decoded draws in
+    test_gpu_pinecones) equals the reference's grid and fire age; the wind index too. Near-ties of an f64
+    uniform against the f32 probability are the only allowed exception."""
+    from gymca_amd.forest_fire.operators import PartiallyObservableForestFire
+    from oracle import alexandridis_classic as cl
+    from test_pinecones_classic_oracle import _classic_fixture_steps
+
+    d = golden("alexandridis_classic")
+    n = checked = 0
+    for key, ctx, grid, draws, _pine, (eg, ea, ew), pine_hits in _classic_fixture_steps(d):
+        op = PartiallyObservableForestFire(0, 1, 2, pinecones=False)
+        H, W = grid.shape
+        dr = dict(draws, burn=draws["burn"].astype(np.float32), grow=draws["grow"].astype(np.float32))
+        new_grid, out_ctx, probs = op(grid.astype(np.int64), None, ctx, draws=dr, return_probs=True)
+        keep = pine_hits == 0
+        diff = (new_grid != eg) & keep
+        if diff.any():  # only where a recorded uniform lies within f32 rounding of the probability
+            u = draws["burn"].reshape(H, W, 9)[..., [0, 1, 2, 3, 5, 6, 7, 8]]
+            assert np.all(np.abs(u - probs).min(axis=-1)[diff] < 1e-6), key
+        assert np.array_equal(np.asarray(out_ctx["fire_age"])[keep & ~diff], ea[keep & ~diff]), key
+        assert int(out_ctx["wind_index"]) == ew, key
+        n, checked = n + 1, checked + int(keep.sum())
+    assert n == 38 and checked > 10000

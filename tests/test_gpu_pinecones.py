@@ -94,7 +94,7 @@ def _classic_case(E, H, W, seed, fire_frac):
 
 @pytest.mark.parametrize("E,H,W,seed,fire_frac", [(3, 24, 24, 1, 0.4), (2, 37, 45, 2, 0.6), (2, 64, 64, 3, 0.5),
                                                   (1, 256, 256, 4, 0.3), (2, 512, 512, 5, 0.15),
-                                                  (1, 600, 580, 6, 0.35)])
+                                                  (1, 600, 580, 6, 0.35), (1, 640, 512, 7, 0.2)])  # 640x512: just above the LDS limit
 def test_classic_pinecones_bit_exact_vs_sequential_oracle(device, E, H, W, seed, fire_frac):
     """gca_alex_pinecones_classic (parallel fixed point of the skip list, LDS bitmaps up to 512^2, the scratch
     path at 600 x 580) == the C oracle's literal sequential loop: grid, ages, counts."""

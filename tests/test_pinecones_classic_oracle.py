@@ -96,3 +96,36 @@ def test_classic_tables_follow_their_laws():
         ks, law = thrust_law(f, K)
         pk = np.diff(np.concatenate([[0.0], t[1:1 + 2 * K].astype(np.float64) / 2 ** 32, [1.0]]))
         assert np.all(np.abs(pk - law) <= 2 ** -31)
+
+
+def _classic_fixture_steps(d):
+    """(context, grid, draws, pine draws, expected grid / age / wind, pinecone-ignited mask) per captured step."""
+    for ci in range(int(d["n"])):
+        base = {k: d[f"c{ci}_{k}"] for k in ("winds", "density", "vegetation", "slope")}
+        p_tree, p_wc = d[f"c{ci}_p"]
+        for t in range(int(d[f"c{ci}_steps"])):
+            pre = f"c{ci}_s{t}_"
+            ctx = dict(base, wind_index=int(d[pre + "wind"]), fire_age=d[pre + "age"].copy(), p_tree=float(p_tree),
+                       p_wind_change=float(p_wc), altitude=np.zeros(d[pre + "grid"].shape))
+            draws = {"burn": d[pre + "burn"], "grow": d[pre + "grow"], "age": d[pre + "draw_age"],
+                     "wind_u": d[pre + "wind_u"], "wind_k": int(d[pre + "wind_k"])}
+            pine = {"n": d[pre + "pine_n"], "dirs": d[pre + "pine_dirs"], "thrust": d[pre + "pine_thrust"],
+                    "u": d[pre + "pine_u"], "age": d[pre + "pine_age"]}
+            yield (ci, t), ctx, d[pre + "grid"], draws, pine, (d[pre + "out_grid"], d[pre + "out_age"],
+                                                               int(d[pre + "out_wind"])), d[pre + "pine_hits"]
+
+
+def test_classic_oracle_matches_the_reference_run(golden):
+    """oracle/alexandridis_classic.update == the reference's own PartiallyObservableForestFire.update loop
+    (ca_alexandridis.py:135-221, run with jax.numpy -> numpy by tests/golden/make_golden.py, every draw recorded):
+    grid, fire ages and wind index bit for bit over 38 consecutive steps of 4 cases (16x16 .. 32x32), with
+    thousands of pinecone ignitions and skip-list events (:151-152, :209-210)."""
+    d = golden("alexandridis_classic")
+    steps = skips = hits = 0
+    for key, ctx, grid, draws, pine, (eg, ea, ew), pine_hits in _classic_fixture_steps(d):
+        ng, na, nw, _, sk = cl.update(grid, ctx, draws, 0, 1, 2, pine=pine)
+        assert np.array_equal(ng, eg), key
+        assert np.array_equal(na, ea), key
+        assert nw == ew, key
+        steps, skips, hits = steps + 1, skips + sk, hits + int(pine_hits.sum())
+    assert steps == 38 and skips > 100 and hits > 1000
