@@ -45,7 +45,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
     ap.add_argument("--size", type=int, default=256)
-    ap.add_argument("--gather", choices=["step", "none"], default="step")
+    ap.add_argument("--gather", choices=["async", "step", "none"], default="async",
+                    help="N > 1: the per-step RCCL all-gather of the episode stats on a side stream overlapping the "
+                         "next step (async), inline (step), or none")
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -125,7 +127,7 @@ def dry_run(args):
     done = (gid % 3 == 0).to(torch.uint8)
     ret = -gid.to(torch.float32) / 8
     length = gid.to(torch.int32) + 1
-    d, r, ln = gd.all_gather_stats(done, ret, length)
+    d, r, ln = (x.reshape(-1) for x in gd.all_gather_stats(done, ret, length))
     allid = torch.arange(total)
     ok = (torch.equal(d, (allid % 3 == 0).to(torch.uint8)) and torch.equal(r, -allid.to(torch.float32) / 8)
           and torch.equal(ln, allid.to(torch.int32) + 1))
@@ -223,6 +225,8 @@ def bench_alex(args, world, rank, device, pg):
     st = dev.stream_ptr(device)
     from gymca_amd import distributed as gd
 
+    stats = gd.StatsGather(E, device, group=None, len_dtype=torch.float32) if world > 1 else None
+
     def step(events):
         call("gca_random_actions", dev.ptr(action), E, env.env_offset, 7, dev.ptr(env.rng_step), st)
         if events is not None:
@@ -234,9 +238,10 @@ def bench_alex(args, world, rank, device, pg):
         else:
             env.ca_step()
         env.post_step(action, stats=True)  # + info steps_elapsed / reward_accumulated, fused
-        if world > 1 and args.gather == "step":
-            # RCCL all-gather of the per-env episode stats (done u8 | return f32 | length i32)
-            gd.all_gather_stats(env.done, env.reward_accumulated, env.steps_elapsed)
+        if stats is not None and args.gather != "none":
+            # RCCL all-gather of the per-env episode stats (return f32 | length f32 | done u8): one
+            # pack + one all_gather_into_tensor into a reused buffer, on a side stream under the next step (async)
+            stats.gather(env.done, env.reward_accumulated, env.steps_elapsed, async_op=args.gather == "async")
 
     detail = {}
     prep = lambda: synthetic_state(env, rank, device)  # every repetition times K steps from the C3 state
@@ -459,9 +464,11 @@ def bench_windy512(args, world, rank, device, pg):
              dev.stream_ptr(device))
         env.step(action)
 
-    def gather():
-        if world > 1:  # RCCL all-gather of done u8 | reward f32 | length i32 per env (gymca_amd.distributed)
-            gd.all_gather_stats(env.done, env.reward, env.steps_elapsed)
+    stats = gd.StatsGather(E, device, len_dtype=env.steps_elapsed.dtype) if world > 1 else None
+
+    def gather(async_op=False):
+        if stats is not None:  # RCCL all-gather of reward f32 | length | done u8 per env (gymca_amd.distributed)
+            stats.gather(env.done, env.reward, env.steps_elapsed, async_op=async_op)
 
     K = max(args.steps, 40)
 
@@ -469,7 +476,12 @@ def bench_windy512(args, world, rank, device, pg):
         one_step()
         gather()
 
+    def overlapped(ev):
+        one_step()
+        gather(async_op=True)
+
     dt_eager, _ = timed_loop(eager, K, args.warmup, pg, device)
+    dt_async, _ = timed_loop(overlapped, K, args.warmup, pg, device)
     G = 8
     graph = StepGraph(one_step, n_steps=G, device=device)
 
@@ -485,8 +497,10 @@ def bench_windy512(args, world, rank, device, pg):
     return {"config": "ForestFireBulldozer 512x512, 1024 envs/GPU (BASELINE config 5 at 8 GPUs), WindyForestFire",
             "env_steps_per_s": world * E * Kg * G / dt_g,
             "env_steps_per_s_eager_gather_every_step": world * E * K / dt_eager,
-            "gather": ("RCCL all_gather of done u8 | reward f32 | length i32 per env (gymca_amd.distributed), "
-                       f"world {world}") if world > 1 else "none (1 GPU)",
+            "env_steps_per_s_async_gather_every_step": world * E * K / dt_async,
+            "gather": ("RCCL all_gather_into_tensor of reward f32 | length | done u8 per env into a reused buffer "
+                       f"(gymca_amd.distributed.StatsGather: 1 pack + 1 collective), world {world}")
+                      if world > 1 else "none (1 GPU)",
             "ca_only_cell_updates_per_s": world * E * N * N / ca["kernel_s"],
             "ca_kernel_ms": ca["kernel_s"] * 1e3,
             "ca_achieved_gbs": WINDY_BYTES_PER_CELL * E * N * N / ca["kernel_s"] / 1e9,
@@ -859,8 +873,9 @@ def main():
             "config": {"workload": "AdvancedForestFireBulldozer 256x256, 4096 envs/GPU, Alexandridis rule, "
                                    "use_hidden=False (BASELINE config 3)",
                        "envs_per_gpu": args.envs, "grid": [args.size, args.size],
-                       "parallelism": f"env-sharded x{world}" + (", RCCL all_gather of done/return/length per step"
-                                                                  if world > 1 and args.gather == "step" else "")},
+                       "parallelism": f"env-sharded x{world}" + (
+                           f", RCCL all_gather of done/return/length per step ({args.gather})"
+                           if world > 1 and args.gather != "none" else "")},
             "rccl_world": world if pg is not None else None,
             "envs_total": world * args.envs,
             "timing": dict(alex["timing"], note="value / ms_per_step = the median of the repetitions, each "

@@ -41,6 +41,7 @@ class EpisodeStats:
         self.ret = torch.zeros(num_envs, dtype=torch.float32, device=device)
         self.len = torch.zeros(num_envs, dtype=torch.int32, device=device)
         self.group = group
+        self._gather = StatsGather(num_envs, device, group=group)
 
     def update(self, reward, done):
         self.ret += reward.to(torch.float32)
@@ -53,24 +54,95 @@ class EpisodeStats:
         return finished_ret, finished_len
 
     def gather(self, done, finished_ret, finished_len):
-        """All ranks' (done u8[E], return f32[E], length i32[E]) concatenated in rank order."""
-        return all_gather_stats(done, finished_ret, finished_len, self.group)
+        """All ranks' (done u8, return f32, length i32), each (world, E) in rank order (views of a reused
+        buffer, valid until the next gather on the same buffer)."""
+        return self._gather.gather(done, finished_ret, finished_len)
+
+
+class StatsGather:
+    """The per-env episode-statistics all-gather, preallocated and reused: per call ONE pack (a single torch.cat
+    of the three fields' bytes into a payload row) and ONE all_gather_into_tensor into a [world, row] byte buffer;
+    no allocation, no host sync, so a step loop can run it eagerly, on a side stream (`async_op=True`,
+    overlapping the next step) or capture it.
+
+    Row layout (bytes): [ret f32 x E | length (4-byte dtype) x E | done u8 x E | pad to a multiple of 4]; the
+    results are strided (world, E) views of the gathered buffer (the 4-byte fields stay aligned for any E).
+    `buffers` payload / result pairs rotate so that an asynchronous gather never has its payload overwritten by
+    the next pack (the pack waits for the gather that last used its buffer). With one rank the pack writes the
+    result row directly: one launch, no collective.
+    """
+
+    def __init__(self, num_envs, device, group=None, buffers=2, len_dtype=torch.int32):
+        E = int(num_envs)
+        self.E = E
+        self.device = torch.device(device)
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.pad = (-E) % 4
+        self.row = 9 * E + self.pad
+        self.len_dtype = len_dtype
+        self._zero_pad = torch.zeros(self.pad, dtype=torch.uint8, device=self.device)
+        self.out = [torch.zeros((self.world, self.row), dtype=torch.uint8, device=self.device) for _ in range(buffers)]
+        # one rank: the pack writes the result row itself; several: a payload the collective reads
+        self.payload = [o[0] if self.world == 1 else torch.zeros(self.row, dtype=torch.uint8, device=self.device)
+                        for o in self.out]
+        self._views = [self._make_views(o) for o in self.out]
+        self._events = [None] * buffers
+        self.k = 0
+        self.stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" and self.world > 1 else None
+
+    def _make_views(self, o):
+        E = self.E
+        return (o[:, 8 * E:9 * E], o[:, :4 * E].view(torch.float32), o[:, 4 * E:8 * E].view(self.len_dtype))
+
+    def gather(self, done, ret, length, async_op=False):
+        """(done u8, ret f32, length) (world, E) views of this call's gathered buffer. async_op=True (CUDA, world >
+        1): the collective runs on a side stream and the returned event must be waited on (event.wait() on the
+        consuming stream) before the views are read: returns (done, ret, length, event)."""
+        E = self.E
+        if ret.dtype != torch.float32 or length.element_size() != 4 or done.element_size() != 1:
+            raise ValueError("gather takes ret f32, a 4-byte length and a 1-byte done flag")
+        if length.dtype != self.len_dtype:
+            self.len_dtype = length.dtype
+            self._views = [self._make_views(o) for o in self.out]
+        if ret.numel() != E or length.numel() != E or done.numel() != E:
+            raise ValueError(f"gather sized for {E} envs per rank")
+        k = self.k
+        self.k = (k + 1) % len(self.out)
+        on_cuda = self.device.type == "cuda"
+        if on_cuda and self._events[k] is not None:  # the side stream's last gather of this buffer is done
+            torch.cuda.current_stream(self.device).wait_event(self._events[k])
+        parts = [ret.reshape(-1).view(torch.uint8), length.reshape(-1).view(torch.uint8),
+                 done.reshape(-1).view(torch.uint8)]
+        if self.pad:
+            parts.append(self._zero_pad)
+        torch.cat(parts, out=self.payload[k])  # the one pack
+        event = None
+        if self.world > 1:
+            flat = self.out[k].view(-1)
+            if async_op and self.stream is not None:
+                self.stream.wait_stream(torch.cuda.current_stream(self.device))
+                with torch.cuda.stream(self.stream):
+                    dist.all_gather_into_tensor(flat, self.payload[k], group=self.group)
+                    event = torch.cuda.Event()
+                    event.record(self.stream)
+                self._events[k] = event
+            else:
+                dist.all_gather_into_tensor(flat, self.payload[k], group=self.group)
+        d, r, ln = self._views[k]
+        return (d, r, ln, event) if async_op else (d, r, ln)
+
+
+_GATHERS = {}
 
 
 def all_gather_stats(done, ret, length, group=None):
-    """One all_gather of a packed [ret f32 | len i32 | done u8] byte buffer (9 bytes per env; the 4-byte
-    fields first so their views stay aligned for any env count)."""
-    E = done.numel()
-    payload = torch.cat([ret.reshape(-1).to(torch.float32).view(torch.uint8),
-                         length.reshape(-1).to(torch.int32).view(torch.uint8), done.reshape(-1).to(torch.uint8)])
-    if not dist.is_initialized() or dist.get_world_size(group) == 1:
-        parts = [payload]
-    else:
-        parts = [torch.empty_like(payload) for _ in range(dist.get_world_size(group))]
-        dist.all_gather(parts, payload, group=group)
-    dones, rets, lens = [], [], []
-    for part in parts:
-        rets.append(part[:4 * E].view(torch.float32))
-        lens.append(part[4 * E:8 * E].view(torch.int32))
-        dones.append(part[8 * E:9 * E])
-    return torch.cat(dones), torch.cat(rets), torch.cat(lens)
+    """One all-gather of the per-env (done u8, return f32, length) of every rank: (world, E) views in rank order
+    (9 bytes per env on the wire), through a StatsGather kept per (E, device, group) — no per-call allocation.
+    The views are valid until the next call with the same shapes rotates back to their buffer."""
+    key = (done.numel(), str(done.device), id(group))
+    g = _GATHERS.get(key)
+    if g is None:
+        g = _GATHERS[key] = StatsGather(done.numel(), done.device, group=group, len_dtype=length.dtype)
+    return g.gather(done, ret, length)

@@ -28,9 +28,34 @@ def _worker(rank, world, port, q):
     # uneven shards are padded to the largest shard before gathering
     E = max(shard(7, world, r)[1] for r in range(world))
     pad = E - n
-    d, r, l = all_gather_stats(torch.cat([done, torch.zeros(pad, dtype=torch.uint8)]),
-                               torch.cat([ret, torch.zeros(pad)]), torch.cat([ln, torch.zeros(pad, dtype=torch.int32)]))
-    q.put((rank, d.tolist(), r.tolist(), l.tolist()))
+    done = torch.cat([done, torch.zeros(pad, dtype=torch.uint8)])
+    ret, ln = torch.cat([ret, torch.zeros(pad)]), torch.cat([ln, torch.zeros(pad, dtype=torch.int32)])
+    d, r, l = all_gather_stats(done, ret, ln)
+    assert d.shape == (world, E)  # (world, E) views of the gathered buffer
+    # the reused StatsGather: no allocation and two ops (the pack, the collective) per call
+    from gymca_amd.distributed import StatsGather
+
+    g = StatsGather(E, "cpu", len_dtype=torch.int32)
+    g.gather(done, ret, ln)  # warm
+    with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU], profile_memory=True) as prof:
+        for _ in range(3):
+            gd, gr, gl = g.gather(done, ret, ln)
+    ops = [e for e in prof.events() if e.name in ("aten::cat", "c10d::_allgather_base_", "c10d::allgather_")
+           or "all_gather" in e.name or "allgather" in e.name]
+
+    def in_collective(e):  # gloo's own staging inside the collective (RCCL has none) is not ours
+        while e is not None:
+            if e.name.startswith("c10d::") or e.name.startswith("gloo:"):
+                return True
+            e = e.cpu_parent
+        return False
+
+    main = {e.thread for e in prof.events() if e.name == "aten::cat"}  # gloo's worker threads are not ours
+    allocs = [e for e in prof.events() if getattr(e, "cpu_memory_usage", 0) > 0 and not in_collective(e)
+              and e.thread in main]
+    q.put((rank, d.reshape(-1).tolist(), r.reshape(-1).tolist(), l.reshape(-1).tolist(),
+           sorted({e.name for e in ops}), len([e for e in ops if e.name == "aten::cat"]), len(allocs),
+           gd.reshape(-1)[:n].tolist() if rank == 0 else None))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -54,7 +79,10 @@ def test_gloo_world2_all_gather_of_episode_stats():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    res = {r: (d, ret, ln) for r, d, ret, ln in out}
+    for _, _, _, _, names, n_cat, n_alloc, _ in out:
+        assert n_cat == 3 and n_alloc == 0, (names, n_cat, n_alloc)  # 3 calls: one pack each, nothing allocated
+        assert any("gather" in nm for nm in names), names
+    res = {r: (d, ret, ln) for r, d, ret, ln, *_ in out}
     assert res[0] == res[1]
     d, ret, ln = res[0]
     # rank 0 holds envs 0..3, rank 1 holds 4..6 (+1 pad)
@@ -86,6 +114,8 @@ def test_all_gather_stats_any_env_count():
     for E in (1, 3, 5, 1023):
         done = (torch.arange(E) % 2).to(torch.uint8)
         d, r, ln = all_gather_stats(done, -torch.arange(E, dtype=torch.float32), torch.arange(E, dtype=torch.int32))
+        assert d.shape == (1, E)
+        d, r, ln = d[0], r[0], ln[0]
         assert torch.equal(d, done) and torch.equal(r, -torch.arange(E, dtype=torch.float32))
         assert torch.equal(ln, torch.arange(E, dtype=torch.int32))
 
