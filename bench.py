@@ -217,8 +217,7 @@ def bench_alex(args, world, rank, device, pg):
     E, N = args.envs, args.size
     env = AdvancedForestFireBulldozerEnv(N, N, key=1, num_envs=E, use_hidden=False, device=device,
                                          env_offset=rank * E, slope_layout=args.slope_layout, observation="rgb",
-                                         enable_extensions=os.environ.get("GCA_BENCH_EXT", "1") != "0",
-                                         tile_skip=args.tile_skip)
+                                         enable_extensions=False, tile_skip=args.tile_skip)
     env.reset()
     synthetic_state(env, rank, device)
     action = torch.zeros((E, 2), dtype=torch.int32, device=device)
@@ -259,25 +258,33 @@ def bench_alex(args, world, rank, device, pg):
     }
     if args.headline_only:
         return res
-    # the full reference env step: + the RGB observation (gca_adv_observation, 12 B/cell of f32 RGB
-    # written), extension choice 1 (unblur) in every env
-    action3 = torch.zeros((E, 3), dtype=torch.int32, device=device)
-    action3[:, 2] = 1
+    # the full reference env step: + the RGB observation of stateless_step (advanced_bulldozer.py:1120). The reference's
+    # default env (enable_extensions=False) gets it from the CA step's own epilogue (gca_alex_step_packed_rgb: 12 B/cell
+    # of f32 RGB written, no second pass) + the bulldozer's pixel (gca_obs_position)
+    fused = env.fused_observation  # the packed layout (the default); --slope-layout edge / planes: its own pass
 
     def step_rgb(events):
-        step(None)
+        call("gca_random_actions", dev.ptr(action), E, env.env_offset, 7, dev.ptr(env.rng_step), st)
         if events is not None:
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record()
-            env.render_observation(action3)
+            env.ca_step(render=fused)
+            if not fused:
+                env.render_observation(None)
             b.record()
             events.append((a, b))
         else:
-            env.render_observation(action3)
+            env.ca_step(render=fused)
+            if not fused:
+                env.render_observation(None)
+        env.post_step(action, stats=True)
+        if fused:
+            call("gca_obs_position", env.obs_params, E, N, N, dev.ptr(env.pos), dev.ptr(env.is_night),
+                 dev.ptr(env.time_step), dev.ptr(env.rgb), st)
 
     dt_rgb, kern_rgb = timed_loop(step_rgb, args.steps, args.warmup, pg, device, reps=3, prepare=prep)
 
-    def step_fill(events):  # the same loop with a write-only fill_ of the RGB buffer in place of the observation
+    def step_fill(events):  # the headline loop with a write-only fill_ of the RGB buffer beside it
         step(None)
         if events is not None:
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -289,13 +296,43 @@ def bench_alex(args, world, rank, device, pg):
             env.rgb.fill_(0.5)
 
     _, kern_fill = timed_loop(step_fill, args.steps, args.warmup, pg, device, reps=1, prepare=prep)
+    # the extension pipeline (enable_extensions=True, extension choice 1 = unblur in every env: blur + visibility):
+    # its own observation pass (gca_adv_observation, 14 B/cell)
+    from gymca_amd.forest_fire.bulldozer.observation import make_obs_params
+
+    plain_params = env.obs_params
+    env.obs_params = make_obs_params(0, 1, 2, True, True, env._day_length)
+    action3 = torch.zeros((E, 3), dtype=torch.int32, device=device)
+    action3[:, 2] = 1
+
+    def step_ext(events):
+        step(None)
+        if events is not None:
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            env.render_observation(action3)
+            b.record()
+            events.append((a, b))
+        else:
+            env.render_observation(action3)
+
+    dt_ext, kern_ext = timed_loop(step_ext, args.steps, args.warmup, pg, device, reps=3, prepare=prep)
+    env.obs_params = plain_params
     res["with_rgb_observation"] = {"env_steps_per_s": world * E * args.steps / dt_rgb,
                                    "cell_updates_per_s": world * E * N * N * args.steps / dt_rgb,
-                                   "obs_kernel_ms": kern_rgb * 1e3,
-                                   "obs_gbs": 14 * E * N * N / kern_rgb / 1e9,
+                                   "ms_per_step": dt_rgb / args.steps * 1e3,
+                                   "fused": fused,
+                                   "step_and_frame_kernels_ms": kern_rgb * 1e3,
+                                   "observation_cost_ms": (kern_rgb - kern) * 1e3,
                                    "same_buffer_fill_ms": kern_fill * 1e3,
-                                   "obs_frac_of_fill": kern_fill / kern_rgb,
-                                   "note": "RGB f32 observation per step like the reference's stateless_step"}
+                                   "note": "the reference's default env step (stateless_step renders RGB f32, "
+                                           "enable_extensions=False): the frame from the CA step's epilogue"}
+    res["with_rgb_observation_extensions"] = {"env_steps_per_s": world * E * args.steps / dt_ext,
+                                              "ms_per_step": dt_ext / args.steps * 1e3,
+                                              "obs_kernel_ms": kern_ext * 1e3,
+                                              "obs_gbs": 14 * E * N * N / kern_ext / 1e9,
+                                              "obs_frac_of_fill": kern_fill / kern_ext,
+                                              "note": "enable_extensions=True, unblur chosen: its own pass"}
     # the same env from its reset state (two burning cells per env, advanced_bulldozer.py:650-688): a
     # real episode's first steps, where the fire-sparsity skip leaves most waves the 7 B/cell of
     # grid/age/dousing traffic. Reported separately; the headline above is the dense mid-episode state.

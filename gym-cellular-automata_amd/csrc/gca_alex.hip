@@ -174,7 +174,23 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 __host__ __device__ constexpr int cp_bytes(int RR, bool pk) {
     return (GCA_ALEX_GLDS && pk && 4 * (RR + 1) * CWP < 32768) ? 32768 : 4 * (RR + 1) * CWP;
 }
-template <int R, int MODE, bool FAST, bool ES, bool PK = false>
+// OBS colour table: after the column prefix, the fire bitmask and the 16-float LUT, 16-B aligned (6 float4)
+__host__ __device__ constexpr int obs_col_off(int RR, bool pk) {
+    return (cp_bytes(RR, pk) + 2 * RR * (TW + 32) / 16 + 64 + 15) & ~15;
+}
+// OBS (PK only): the step also writes the env's RGB observation of the plain case (no extension channel, no grid
+// transform — advanced_bulldozer.py:1035-1101 with enable_extensions=False, the reference's default): every cell's
+// colour is a function of its NEW state (grid_to_rgb of the post-step grid, :1120) and its PRE-step dousing bit and
+// day / night (the MDP renders with the input per_env_context, :1121) — all of which this kernel holds — so the
+// frame costs its 12 B/cell of writes and nothing else. The bulldozer's pixel (:1099) is written afterwards by
+// gca_obs_position (the position is only known after the env step's Move).
+struct AlexObs {
+    const float4* col;       // [2 nights][3 kinds][2 dousing] colours (gca_obs_color_table)
+    const int32_t* night;    // [E] pre-step is_night
+    float* rgb;              // [E][H][W][3]
+};
+
+template <int R, int MODE, bool FAST, bool ES, bool PK = false, bool OBS = false>
 __global__ __launch_bounds__(NT, GCA_ALEX_WGS) void alex_step_kernel(
     gca_alex_params p, int H, int W, int tiles_r, int tiles_c, const uint8_t* __restrict__ grid_in,
     uint8_t* __restrict__ grid_out, const int16_t* age_in, int16_t* age_out,  // no __restrict__: PK updates in place
@@ -182,7 +198,8 @@ __global__ __launch_bounds__(NT, GCA_ALEX_WGS) void alex_step_kernel(
     const float* __restrict__ p_slope, const int32_t* __restrict__ wind_index, const uint32_t* __restrict__ rng_step,
     const float* __restrict__ inj_burn, const float* __restrict__ inj_grow, const int32_t* __restrict__ inj_age,
     float* __restrict__ prob_out, int32_t* __restrict__ counts, const uint8_t* __restrict__ act_in,
-    uint8_t* __restrict__ act_out) {
+    uint8_t* __restrict__ act_out, AlexObs obs) {
+    static_assert(!OBS || PK, "the fused observation runs on the packed env layout");
     constexpr bool INJECT = MODE == 2;
     constexpr bool PROB = MODE != 0;
     constexpr int RS = R < 2 ? 2 : R;  // staged halo: heat radius, at least the 5x5 dousing box
@@ -194,6 +211,8 @@ __global__ __launch_bounds__(NT, GCA_ALEX_WGS) void alex_step_kernel(
     uint16_t* FB = reinterpret_cast<uint16_t*>(smem + CPB);                                  // [RR][NCH] fire bits
     float* LUT = reinterpret_cast<float*>(smem + CPB + sizeof(uint16_t) * RR * NCH);
     // LUT[0..7] = 1 + p_veg[clip(v, 1, 5)] for v = min(byte, 7); LUT[8..15] the same for density
+    float4* COL = reinterpret_cast<float4*>(smem + obs_col_off(RR, PK));
+    static_assert(!OBS || cp_bytes(RR, PK) >= 4 * 6144, "OBS: 6 KiB of dead column prefix per wave");  // OBS: the env's 6 colours (kind x dousing)
 
     // XCD-aware order: blocks b, b+8, b+16, ... share an XCD (and its L2) under round-robin
     // dispatch; give each XCD a contiguous range of (env, tile) so the halo rows a tile stages
@@ -369,6 +388,59 @@ __global__ __launch_bounds__(NT, GCA_ALEX_WGS) void alex_step_kernel(
                 if (row_ok && cbase + i < W) agew[i >> 1] |= (uint32_t)(uint16_t)aEi[lo + i] << (16 * (i & 1));
         }
     };
+    // ---- OBS epilogue: RGB f32 of the lane's 16 cells (tB / fB: new TREE / FIRE masks, bit i <-> cell i) through a
+    //      per-wave transposition in the column-prefix LDS (dead after the heat phase: a workgroup barrier orders every
+    //      wave's reads before the first write), two rounds of two image rows, so that every non-temporal store
+    //      instruction writes 1 KiB of contiguous RGB (per-lane 192-B stores were 4x slower in gca_obs.hip, r01m)
+    auto write_rgb = [&](uint32_t tB, uint32_t fB) {
+        if constexpr (OBS) {
+            if (tid < 6) {
+                const int nt = obs.night[e] != 0 ? 1 : 0;
+                COL[tid] = obs.col[6 * nt + tid];
+            }
+            const uint32_t dbits = dbE[lo >> 4];  // PRE-step dousing bits of this lane's 16 cells
+            __syncthreads();
+            const int lane = tid & 63, wv = tid >> 6;
+            float4* img = reinterpret_cast<float4*>(smem) + wv * 384;  // 6 KiB per wave
+            typedef float f4t __attribute__((ext_vector_type(4)));
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                if ((lane >> 5) == h) {  // lanes 32h .. 32h+31 hold this wave's image rows 2h, 2h+1
+                    float4* dst = img + ((lane >> 4) & 1) * 192 + q * 12;
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        float c[12];
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const int i = 4 * g + j;
+                            const int kind = ((tB >> i) & 1u) ? 1 : (((fB >> i) & 1u) ? 2 : 0);
+                            const float4 cl = COL[2 * kind + (int)((dbits >> i) & 1u)];
+                            c[3 * j] = cl.x;
+                            c[3 * j + 1] = cl.y;
+                            c[3 * j + 2] = cl.z;
+                        }
+                        dst[3 * g] = make_float4(c[0], c[1], c[2], c[3]);
+                        dst[3 * g + 1] = make_float4(c[4], c[5], c[6], c[7]);
+                        dst[3 * g + 2] = make_float4(c[8], c[9], c[10], c[11]);
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+                for (int jj = 0; jj < 6; ++jj) {
+                    const int lr = jj / 3;  // image row of the round (3 x 1 KiB per 256-column row segment)
+                    const int row = r0 + 4 * wv + 2 * h + lr;
+                    float* gdst = obs.rgb + (((size_t)e * H + row) * W + c0) * 3 + 4 * (64 * (jj - 3 * lr) + lane);
+                    const float4 v = img[64 * jj + lane];
+                    __builtin_nontemporal_store((f4t){v.x, v.y, v.z, v.w}, reinterpret_cast<f4t*>(gdst));
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // this round's reads before the next writes
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+        }
+    };
     // ---------------- stage rows [r0-RS, r0+TH+RS) x cols [c0-16, c0+TW+16):
     //                  packed fire | dousing<<16 -> CP rows 1..RR, fire bitmask -> FB
     //                  every load of the thread's chunks is issued before any is processed
@@ -456,6 +528,12 @@ __global__ __launch_bounds__(NT, GCA_ALEX_WGS) void alex_step_kernel(
                         if (cE) atomicAdd(counts + 3 * e + 0, cE);
                         if (cT) atomicAdd(counts + 3 * e + 1, cT);
                     }
+                }
+                if constexpr (OBS) {  // the copied tile has no FIRE (it holds none and none reaches it)
+                    uint32_t tB = 0u;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) tB |= eq_nib(own[j], Tp) << (4 * j);
+                    write_rgb(tB, 0u);
                 }
                 return;  // the whole workgroup (anyf is workgroup-uniform)
             }
@@ -1006,6 +1084,7 @@ __global__ __launch_bounds__(NT, GCA_ALEX_WGS) void alex_step_kernel(
             }
         }
     }
+    write_rgb(newT, newF);
     if (counts || (PK && act_out)) {
         int cntT = __builtin_popcount(newT & okB), cntF = __builtin_popcount(newF & okB),
             cntE = __builtin_popcount(newE & okB);
@@ -1041,37 +1120,42 @@ __global__ void alex_prepare_slope_kernel(const float* __restrict__ slope, float
     }
 }
 
-template <int R, int MODE, bool ES, bool PK = false>
+template <int R, int MODE, bool ES, bool PK = false, bool OBS = false>
 void launch_alex(const gca_alex_params& p, int E, int H, int W, const uint8_t* gi, uint8_t* go, const int16_t* ai,
                  int16_t* ao, const uint8_t* veg, const uint8_t* den, const uint8_t* dous, const float* ps,
                  const int32_t* wi, const uint32_t* rs, const float* ib, const float* ig, const int32_t* ia, float* po,
-                 int32_t* counts, hipStream_t st, const uint8_t* act_in = nullptr, uint8_t* act_out = nullptr) {
+                 int32_t* counts, hipStream_t st, const uint8_t* act_in = nullptr, uint8_t* act_out = nullptr,
+                 AlexObs obs = AlexObs{nullptr, nullptr, nullptr}) {
     const int tiles_r = (H + TH - 1) / TH, tiles_c = (W + TW - 1) / TW;
     constexpr int RS = R < 2 ? 2 : R;
     constexpr int RR = TH + 2 * RS;
-    const size_t lds = (size_t)cp_bytes(RR, PK) + sizeof(uint16_t) * RR * (CW / 16) + sizeof(float) * 16;
+    const size_t lds = OBS ? (size_t)obs_col_off(RR, PK) + 6 * sizeof(float4)
+                           : (size_t)cp_bytes(RR, PK) + sizeof(uint16_t) * RR * (CW / 16) + sizeof(float) * 16;
     const dim3 grid((unsigned)((int64_t)E * tiles_r * tiles_c));
     const bool fast = MODE == 0 && W % TW == 0 && H % TH == 0 &&
                       ((((uintptr_t)gi) | ((uintptr_t)go) | ((uintptr_t)ai) | ((uintptr_t)ao) | ((uintptr_t)veg) |
                         ((uintptr_t)den) | ((uintptr_t)dous) | ((uintptr_t)ps)) & 15u) == 0;
     if (PK)  // packed env layout (the host checked the FAST shape and alignment)
-        hipLaunchKernelGGL((alex_step_kernel<R, 0, true, true, true>), grid, dim3(NT), lds, st, p, H, W, tiles_r,
-                           tiles_c, gi, go, ai, ao, veg, den, dous, ps, wi, rs, ib, ig, ia, po, counts, act_in, act_out);
+        hipLaunchKernelGGL((alex_step_kernel<R, 0, true, true, true, OBS>), grid, dim3(NT), lds, st, p, H, W, tiles_r,
+                           tiles_c, gi, go, ai, ao, veg, den, dous, ps, wi, rs, ib, ig, ia, po, counts, act_in, act_out,
+                           obs);
     else if (fast)  // production shape: no per-lane bounds checks (instantiated for the Philox mode only)
         hipLaunchKernelGGL((alex_step_kernel<R, MODE, MODE == 0, ES>), grid, dim3(NT), lds, st, p, H, W, tiles_r,
-                           tiles_c, gi, go, ai, ao, veg, den, dous, ps, wi, rs, ib, ig, ia, po, counts, act_in, act_out);
+                           tiles_c, gi, go, ai, ao, veg, den, dous, ps, wi, rs, ib, ig, ia, po, counts, act_in, act_out,
+                           obs);
     else
         hipLaunchKernelGGL((alex_step_kernel<R, MODE, false, ES>), grid, dim3(NT), lds, st, p, H, W, tiles_r, tiles_c,
-                           gi, go, ai, ao, veg, den, dous, ps, wi, rs, ib, ig, ia, po, counts, act_in, act_out);
+                           gi, go, ai, ao, veg, den, dous, ps, wi, rs, ib, ig, ia, po, counts, act_in, act_out, obs);
 }
 
-template <int MODE, bool ES, bool PK = false>
+template <int MODE, bool ES, bool PK = false, bool OBS = false>
 void dispatch_r(int R, const gca_alex_params& p, int E, int H, int W, const uint8_t* gi, uint8_t* go, const int16_t* ai,
                 int16_t* ao, const uint8_t* veg, const uint8_t* den, const uint8_t* dous, const float* ps,
                 const int32_t* wi, const uint32_t* rs, const float* ib, const float* ig, const int32_t* ia, float* po,
-                int32_t* counts, hipStream_t st, const uint8_t* act_in = nullptr, uint8_t* act_out = nullptr) {
+                int32_t* counts, hipStream_t st, const uint8_t* act_in = nullptr, uint8_t* act_out = nullptr,
+                AlexObs obs = AlexObs{nullptr, nullptr, nullptr}) {
 #define GCA_ALEX_CASE(RV) \
-    case RV: launch_alex<RV, MODE, ES, PK>(p, E, H, W, gi, go, ai, ao, veg, den, dous, ps, wi, rs, ib, ig, ia, po, counts, st, act_in, act_out); break;
+    case RV: launch_alex<RV, MODE, ES, PK, OBS>(p, E, H, W, gi, go, ai, ao, veg, den, dous, ps, wi, rs, ib, ig, ia, po, counts, st, act_in, act_out, obs); break;
     switch (R) {
 #ifdef GCA_ALEX_ONLY_R  // ISA inspection builds: one radius only
         GCA_ALEX_CASE(GCA_ALEX_ONLY_R)
@@ -1115,13 +1199,13 @@ static int alex_step_impl(bool es, const gca_alex_params* p, int E, int H, int W
     }
     if (inj)
         (es ? dispatch_r<2, true> : dispatch_r<2, false>)(p->R, *p, E, H, W, grid_in, grid_out, age_in, age_out, veg, den, dousing, p_slope, wind_index,
-                         rng_step, inj_burn, inj_grow, inj_age, prob_out, counts, st, nullptr, nullptr);
+                         rng_step, inj_burn, inj_grow, inj_age, prob_out, counts, st, nullptr, nullptr, AlexObs{});
     else if (prob_out)
         (es ? dispatch_r<1, true> : dispatch_r<1, false>)(p->R, *p, E, H, W, grid_in, grid_out, age_in, age_out, veg, den, dousing, p_slope, wind_index,
-                      rng_step, nullptr, nullptr, nullptr, prob_out, counts, st, nullptr, nullptr);
+                      rng_step, nullptr, nullptr, nullptr, prob_out, counts, st, nullptr, nullptr, AlexObs{});
     else
         (es ? dispatch_r<0, true> : dispatch_r<0, false>)(p->R, *p, E, H, W, grid_in, grid_out, age_in, age_out, veg, den, dousing, p_slope, wind_index,
-                      rng_step, nullptr, nullptr, nullptr, nullptr, counts, st, nullptr, nullptr);
+                      rng_step, nullptr, nullptr, nullptr, nullptr, counts, st, nullptr, nullptr, AlexObs{});
     GCA_CHECK_LAUNCH(es ? "alex_step_es" : "alex_step");
     return GCA_OK;
 }
@@ -1145,11 +1229,11 @@ extern "C" int gca_alex_step_es(const gca_alex_params* p, int E, int H, int W, c
                           wind_index, rng_step, inj_burn, inj_grow, inj_age, prob_out, counts, stream);
 }
 
-extern "C" int gca_alex_step_packed(const gca_alex_params* p, int E, int H, int W, const uint8_t* grid_in,
-                                    uint8_t* grid_out, const int16_t* age_in, int16_t* age_out, const uint8_t* vd,
-                                    const uint16_t* dous_bits, const float* edge_slope_coal, const int32_t* wind_index,
-                                    const uint32_t* rng_step, int32_t* counts, const uint8_t* act_in, uint8_t* act_out,
-                                    void* stream) {
+static int alex_step_packed_impl(const gca_alex_params* p, int E, int H, int W, const uint8_t* grid_in,
+                                 uint8_t* grid_out, const int16_t* age_in, int16_t* age_out, const uint8_t* vd,
+                                 const uint16_t* dous_bits, const float* edge_slope_coal, const int32_t* wind_index,
+                                 const uint32_t* rng_step, int32_t* counts, const uint8_t* act_in, uint8_t* act_out,
+                                 AlexObs obs, void* stream) {
     GCA_CHECK_ARG(p && grid_in && grid_out && age_in && age_out && vd && dous_bits && edge_slope_coal && wind_index,
                   "alex_step_packed: null argument");
     GCA_CHECK_ARG(E > 0 && H > 0 && W > 0 && W % TW == 0 && H % TH == 0,
@@ -1159,7 +1243,8 @@ extern "C" int gca_alex_step_packed(const gca_alex_params* p, int E, int H, int 
     // ages may be updated in place (each lane reads and writes only its own cells); the grid may not (halos)
     GCA_CHECK_ARG(grid_in != grid_out, "alex_step_packed: the grid cannot be updated in place");
     GCA_CHECK_ARG(((((uintptr_t)grid_in) | ((uintptr_t)grid_out) | ((uintptr_t)age_in) | ((uintptr_t)age_out) |
-                    ((uintptr_t)vd) | ((uintptr_t)edge_slope_coal)) & 15u) == 0 && ((uintptr_t)dous_bits & 1u) == 0,
+                    ((uintptr_t)vd) | ((uintptr_t)edge_slope_coal) | ((uintptr_t)obs.rgb) | ((uintptr_t)obs.col)) & 15u) == 0
+                      && ((uintptr_t)dous_bits & 1u) == 0,
                   "alex_step_packed: arrays must be 16-B aligned");
     hipStream_t st = (hipStream_t)stream;
     if (counts && hipMemsetAsync(counts, 0, sizeof(int32_t) * 3 * (size_t)E, st) != hipSuccess) {
@@ -1170,11 +1255,37 @@ extern "C" int gca_alex_step_packed(const gca_alex_params* p, int E, int H, int 
     GCA_CHECK_ARG(act_in != act_out || !act_in, "alex_step_packed: act_in and act_out must differ");
     // a tile without fire nearby can still change when EMPTY cells grow: the skip needs p_tree == 0
     const uint8_t* ain = (p->p_tree > 0.0f) ? nullptr : act_in;
-    dispatch_r<0, true, true>(p->R, *p, E, H, W, grid_in, grid_out, age_in, age_out, vd, nullptr,
-                              reinterpret_cast<const uint8_t*>(dous_bits), edge_slope_coal, wind_index, rng_step, nullptr,
-                              nullptr, nullptr, nullptr, counts, st, ain, act_out);
-    GCA_CHECK_LAUNCH("alex_step_packed");
+    if (obs.rgb)
+        dispatch_r<0, true, true, true>(p->R, *p, E, H, W, grid_in, grid_out, age_in, age_out, vd, nullptr,
+                                        reinterpret_cast<const uint8_t*>(dous_bits), edge_slope_coal, wind_index, rng_step,
+                                        nullptr, nullptr, nullptr, nullptr, counts, st, ain, act_out, obs);
+    else
+        dispatch_r<0, true, true>(p->R, *p, E, H, W, grid_in, grid_out, age_in, age_out, vd, nullptr,
+                                  reinterpret_cast<const uint8_t*>(dous_bits), edge_slope_coal, wind_index, rng_step, nullptr,
+                                  nullptr, nullptr, nullptr, counts, st, ain, act_out);
+    GCA_CHECK_LAUNCH(obs.rgb ? "alex_step_packed_rgb" : "alex_step_packed");
     return GCA_OK;
+}
+
+extern "C" int gca_alex_step_packed(const gca_alex_params* p, int E, int H, int W, const uint8_t* grid_in,
+                                    uint8_t* grid_out, const int16_t* age_in, int16_t* age_out, const uint8_t* vd,
+                                    const uint16_t* dous_bits, const float* edge_slope_coal, const int32_t* wind_index,
+                                    const uint32_t* rng_step, int32_t* counts, const uint8_t* act_in, uint8_t* act_out,
+                                    void* stream) {
+    return alex_step_packed_impl(p, E, H, W, grid_in, grid_out, age_in, age_out, vd, dous_bits, edge_slope_coal,
+                                 wind_index, rng_step, counts, act_in, act_out, AlexObs{nullptr, nullptr, nullptr}, stream);
+}
+
+extern "C" int gca_alex_step_packed_rgb(const gca_alex_params* p, int E, int H, int W, const uint8_t* grid_in,
+                                        uint8_t* grid_out, const int16_t* age_in, int16_t* age_out, const uint8_t* vd,
+                                        const uint16_t* dous_bits, const float* edge_slope_coal,
+                                        const int32_t* wind_index, const uint32_t* rng_step, int32_t* counts,
+                                        const uint8_t* act_in, uint8_t* act_out, const float* color_table,
+                                        const int32_t* is_night, float* rgb, void* stream) {
+    GCA_CHECK_ARG(color_table && is_night && rgb, "alex_step_packed_rgb: color_table, is_night and rgb required");
+    return alex_step_packed_impl(p, E, H, W, grid_in, grid_out, age_in, age_out, vd, dous_bits, edge_slope_coal,
+                                 wind_index, rng_step, counts, act_in, act_out,
+                                 AlexObs{reinterpret_cast<const float4*>(color_table), is_night, rgb}, stream);
 }
 
 // ------------------------------------------------------------------ packed env layers

@@ -46,9 +46,10 @@ __device__ __forceinline__ u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1
         const uint64_t p1 = (uint64_t)M1 * c.z;
         const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
         const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
-        uint32_t n0, n2;  // one v_bitop3_b32 (3-input xor, table 0x96) each; the compiler emits two v_xor_b32
-        asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(n0) : "v"(hi1), "v"(c.y), "s"(k0));
-        asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(n2) : "v"(hi0), "v"(c.w), "s"(k1));
+        // one v_bitop3_b32 (3-input xor, table 0x96) each; the builtin (not inline asm) lets the hazard
+        // recogniser and the scheduler see it: inline asm cost an s_nop before every following v_mad_u64_u32
+        const uint32_t n0 = __builtin_amdgcn_bitop3_b32(hi1, c.y, k0, 0x96);
+        const uint32_t n2 = __builtin_amdgcn_bitop3_b32(hi0, c.w, k1, 0x96);
         c = u32x4{n0, lo1, n2, lo0};
         k0 += W0;
         k1 += W1;

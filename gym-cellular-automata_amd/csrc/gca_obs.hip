@@ -481,7 +481,52 @@ __global__ __launch_bounds__(256) void adv_obs_plain_kernel(gca_obs_params p, in
     }
 }
 
+// colour table of the fused step observation (gca_alex_step_packed_rgb): [night][kind][dousing 0 / 1] as float4
+__global__ void obs_color_table_kernel(gca_obs_params p, float4* __restrict__ table) {
+    const int i = (int)threadIdx.x;
+    if (i >= 12) return;
+    float c3[3];
+    render_kind(p, c3, (i % 6) / 2, i % 2, i >= 6);
+    table[i] = make_float4(c3[0], c3[1], c3[2], 0.0f);
+}
+
+// the bulldozer's pixel (grid_to_rgb's .at[position].set, advanced_bulldozer.py:1095-1099) over a frame the fused step
+// wrote: position colour of the PRE-step day / night (the step toggled is_night when time_step % day_length == 0)
+__global__ void obs_position_kernel(gca_obs_params p, int E, int H, int W, const int32_t* __restrict__ pos,
+                                    const int32_t* __restrict__ is_night, const int32_t* __restrict__ time_step,
+                                    float* __restrict__ rgb) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= E) return;
+    bool night = is_night[e] != 0;
+    if (time_step && p.day_length > 0 && time_step[e] % p.day_length == 0) night = !night;
+    const int r = pos[2 * e], c = pos[2 * e + 1];
+    if (r < 0 || r >= H || c < 0 || c >= W) return;  // JAX drops out-of-bounds updates
+    float c3[3];
+    render_kind(p, c3, 3, 0, night);
+    float* o = rgb + (((int64_t)e * H + r) * W + c) * 3;
+    o[0] = c3[0];
+    o[1] = c3[1];
+    o[2] = c3[2];
+}
+
 }  // namespace
+
+extern "C" int gca_obs_color_table(const gca_obs_params* p, float* table, void* stream) {
+    GCA_CHECK_ARG(p && table && ((uintptr_t)table & 15u) == 0, "obs_color_table: bad arguments");
+    hipLaunchKernelGGL(obs_color_table_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, *p,
+                       reinterpret_cast<float4*>(table));
+    GCA_CHECK_LAUNCH("obs_color_table");
+    return GCA_OK;
+}
+
+extern "C" int gca_obs_position(const gca_obs_params* p, int E, int H, int W, const int32_t* pos,
+                                const int32_t* is_night, const int32_t* time_step, float* rgb, void* stream) {
+    GCA_CHECK_ARG(p && pos && is_night && rgb && E > 0 && H > 0 && W > 0, "obs_position: bad arguments");
+    hipLaunchKernelGGL(obs_position_kernel, dim3((E + 255) / 256), dim3(256), 0, (hipStream_t)stream, *p, E, H, W, pos,
+                       is_night, time_step, rgb);
+    GCA_CHECK_LAUNCH("obs_position");
+    return GCA_OK;
+}
 
 extern "C" int gca_adv_observation(const gca_obs_params* p, int mode, int E, int H, int W, const uint8_t* grid,
                                    const uint8_t* dousing, const int32_t* pos, const int32_t* is_night,

@@ -152,6 +152,11 @@ class AdvancedForestFireBulldozerEnv:
         self.obs_params = make_obs_params(self._empty, self._tree, self._fire, self.enable_extensions,
                                           self.enable_extensions, self._day_length)
         self.rgb = torch.zeros((E, H, W, 3), dtype=torch.float32, **kw) if observation == "rgb" else None
+        # the plain observation (no extension channel, no transform: the reference's default) is written by the CA
+        # step itself on the packed layout (gca_alex_step_packed_rgb) and the bulldozer's pixel by gca_obs_position;
+        # extensions, other layouts and pinecones (which ignite cells after the step) render it in its own pass
+        self.obs_colors = torch.zeros((12, 4), dtype=torch.float32, **kw)
+        call("gca_obs_color_table", self.obs_params, dev.ptr(self.obs_colors), dev.stream_ptr(self.device))
         self._build_context_layers(hidden_rng)
 
     # ------------------------------------------------------------------ init
@@ -602,16 +607,29 @@ class AdvancedForestFireBulldozerEnv:
              dev.stream_ptr(self.device))
         return self.rgb
 
-    def ca_step(self):
-        """The CA step alone (RepeatCAJax's one step) for every env; swaps the ping-pong buffers."""
+    @property
+    def fused_observation(self):
+        """True when env.step's RGB observation comes out of the CA step's own epilogue (see __init__)."""
+        return (self.rgb is not None and self.slope_layout == "packed" and not self.enable_extensions
+                and not self.obs_params.should_transform and not self.pinecones)
+
+    def ca_step(self, render=False):
+        """The CA step alone (RepeatCAJax's one step) for every env; swaps the ping-pong buffers. render=True (with
+        fused_observation) also writes the step's RGB frame, all but the bulldozer's pixel."""
         E, H, W = self.num_envs, self.nrows, self.ncols
         a, b = self.cur, 1 - self.cur
         if self.slope_layout == "packed":
-            call("gca_alex_step_packed", self.alex_params, E, H, W, dev.ptr(self.grid[a]), dev.ptr(self.grid[b]),
-                 dev.ptr(self.age[a]), dev.ptr(self.age[b]), dev.ptr(self.vd), dev.ptr(self.dous_bits),
-                 dev.ptr(self.slope_data), dev.ptr(self.wind_index), dev.ptr(self.rng_step), dev.ptr(self.counts),
-                 dev.ptr(None if self.act is None else self.act[a]), dev.ptr(None if self.act is None else self.act[b]),
-                 dev.stream_ptr(self.device))
+            args = (self.alex_params, E, H, W, dev.ptr(self.grid[a]), dev.ptr(self.grid[b]),
+                    dev.ptr(self.age[a]), dev.ptr(self.age[b]), dev.ptr(self.vd), dev.ptr(self.dous_bits),
+                    dev.ptr(self.slope_data), dev.ptr(self.wind_index), dev.ptr(self.rng_step), dev.ptr(self.counts),
+                    dev.ptr(None if self.act is None else self.act[a]), dev.ptr(None if self.act is None else self.act[b]))
+            if render:
+                if not self.fused_observation:
+                    raise ValueError("ca_step(render=True) needs fused_observation")
+                call("gca_alex_step_packed_rgb", *args, dev.ptr(self.obs_colors), dev.ptr(self.is_night),
+                     dev.ptr(self.rgb), dev.stream_ptr(self.device))
+            else:
+                call("gca_alex_step_packed", *args, dev.stream_ptr(self.device))
             self._pinecones(a, b)
             self.cur = b
             return
@@ -635,9 +653,13 @@ class AdvancedForestFireBulldozerEnv:
         """Gymnasium-style step of every env: action (E, 2) or (E, 3) ints (move, shoot[, extension choice]),
         device tensor or numpy. Returns (obs, reward, terminated, truncated, info) like stateless_step."""
         full = self._full_action(action)
-        self.ca_step()
+        fused = self.fused_observation
+        self.ca_step(render=fused)
         self.post_step(full[:, :2].contiguous(), stats=True)
-        if self.rgb is not None:
+        if fused:  # the frame came with the CA step; the bulldozer's pixel at its new position
+            call("gca_obs_position", self.obs_params, self.num_envs, self.nrows, self.ncols, dev.ptr(self.pos),
+                 dev.ptr(self.is_night), dev.ptr(self.time_step), dev.ptr(self.rgb), dev.stream_ptr(self.device))
+        elif self.rgb is not None:
             self.render_observation(full)
         return self._obs(), self.reward, self.done.bool(), self.truncated, self._info()
 

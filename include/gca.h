@@ -183,6 +183,17 @@ int gca_alex_step_packed(const gca_alex_params* p, int E, int H, int W, const ui
                          const int16_t* age_in, int16_t* age_out, const uint8_t* vd, const uint16_t* dous_bits,
                          const float* edge_slope_coal, const int32_t* wind_index, const uint32_t* rng_step,
                          int32_t* counts, const uint8_t* act_in, uint8_t* act_out, void* stream);
+/* gca_alex_step_packed that ALSO writes the env's step observation of the plain case (enable_extensions = False, the
+ * reference's default; advanced_bulldozer.py:1035-1101, :1120): rgb [E][H][W][3] f32 of every cell = the colour of its
+ * NEW state (empty / tree / fire; other codes the empty colour) under the PRE-step is_night[e], water-tinted where its
+ * PRE-step dousing bit is set (the MDP renders with the input per_env_context, :1121) — the frame gca_adv_observation
+ * (mode 0) renders from the same inputs, minus the bulldozer's pixel, which gca_obs_position adds once the env step
+ * has moved it. color_table [2][3][2][4] f32 from gca_obs_color_table (16-B aligned, like rgb). */
+int gca_alex_step_packed_rgb(const gca_alex_params* p, int E, int H, int W, const uint8_t* grid_in, uint8_t* grid_out,
+                             const int16_t* age_in, int16_t* age_out, const uint8_t* vd, const uint16_t* dous_bits,
+                             const float* edge_slope_coal, const int32_t* wind_index, const uint32_t* rng_step,
+                             int32_t* counts, const uint8_t* act_in, uint8_t* act_out, const float* color_table,
+                             const int32_t* is_night, float* rgb, void* stream);
 /* vd (nullable) and dous_bits of gca_alex_step_packed from veg / den / dousing (E,H,W) u8; W % 16 == 0. */
 int gca_alex_pack_layers(const uint8_t* veg, const uint8_t* den, const uint8_t* dousing, uint8_t* vd,
                          uint16_t* dous_bits, int E, int H, int W, void* stream);
@@ -371,6 +382,14 @@ int gca_adv_observation(const gca_obs_params* p, int mode, int E, int H, int W, 
                         const uint8_t* dousing, const int32_t* pos, const int32_t* is_night, const int32_t* time_step,
                         const int32_t* action, int action_stride, float* rgb, uint8_t* channels,
                         const uint8_t* env_mask, void* stream);
+
+/* [night][kind empty / tree / fire][dousing 0 / 1] float4 colours (rgb, 0) of grid_to_rgb (advanced_bulldozer.py:1041-1093),
+ * the table gca_alex_step_packed_rgb reads: table[12][4] f32 device, 16-B aligned. */
+int gca_obs_color_table(const gca_obs_params* p, float* table, void* stream);
+/* rgb[e][pos[e]] = the position colour of the PRE-step day / night (is_night after the env step, time_step to undo its
+ * toggle; time_step NULL = is_night as given): grid_to_rgb's .at[position].set (:1095-1099) over a fused frame. */
+int gca_obs_position(const gca_obs_params* p, int E, int H, int W, const int32_t* pos, const int32_t* is_night,
+                     const int32_t* time_step, float* rgb, void* stream);
 
 /* Synthetic inputs for benches/tests (Philox, GCA_TAG_INIT / GCA_TAG_ACTION). */
 int gca_fill_categorical(uint8_t* out, int64_t n_per_env, int E, int env_offset, uint64_t seed,

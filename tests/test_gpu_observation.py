@@ -104,3 +104,42 @@ def test_env_rgb_observation(device):
             want, _ = ob.step_observation(g[e].astype(np.int32), tuple(pos[e]), EXTENSION_LOOKUP[act[e, 2]],
                                           int(night_pre[e]), dous_pre[e], True, True)
             assert np.array_equal(rgb[e].cpu().numpy(), want), (s, e)
+
+
+@pytest.mark.parametrize("tile_skip", [False, True])
+def test_fused_step_observation_matches_reference(device, tile_skip):
+    """The plain observation (enable_extensions=False, the reference's default) written by the CA step's own
+    epilogue on the packed layout (gca_alex_step_packed_rgb) + the bulldozer's pixel (gca_obs_position) equals the
+    literal restatement of grid_to_rgb (advanced_bulldozer.py:1035-1101) of the post-step grid and position with the
+    PRE-step dousing and day / night: over steps with shooting, a day / night toggle, W = 512 (two tiles per row),
+    the tile-skip path and a conditional reset."""
+    import torch
+
+    from gymca_amd.forest_fire.bulldozer import AdvancedForestFireBulldozerEnv
+
+    E, H, W = 3, 256, 512
+    env = AdvancedForestFireBulldozerEnv(H, W, key=8, num_envs=E, use_hidden=True, device=device, observation="grid",
+                                         hidden_rng="philox", tile_skip=tile_skip)
+    # observation="rgb" needs a square grid for the reset frame; the step frame does not: give this env an RGB buffer
+    env.rgb = torch.zeros((E, H, W, 3), dtype=torch.float32, device=device)
+    assert env.fused_observation
+    env.reset()
+    env.pos[:, 0], env.pos[:, 1] = 190, 60  # near the initial fire: shots land on burning / tree cells
+    env.time_step.fill_(398)
+    rng = np.random.default_rng(4)
+    for s in range(8):
+        night_pre = env.is_night.cpu().numpy().copy()
+        dous_pre = env.dousing.cpu().numpy().astype(np.int32)
+        act = np.stack([rng.integers(0, 9, E), rng.integers(0, 2, E)], axis=1)
+        env.step(act)
+        g = env.grid[env.cur].cpu().numpy()
+        pos = env.pos.cpu().numpy()
+        rgb = env.rgb.cpu().numpy()
+        for e in range(E):
+            want, _ = ob.step_observation(g[e].astype(np.int32), tuple(pos[e]), (0, 0), int(night_pre[e]),
+                                          dous_pre[e], False, False)
+            assert np.array_equal(rgb[e], want), (s, e)
+        if s == 4:
+            env.done[1] = 1
+            env.conditional_reset()
+    assert int(env.dousing.sum()) > 0 and env.is_night.cpu().numpy().any()
