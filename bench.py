@@ -269,18 +269,16 @@ def bench_alex(args, world, rank, device, pg):
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record()
             env.ca_step(render=fused)
-            if not fused:
-                env.render_observation(None)
             b.record()
             events.append((a, b))
         else:
             env.ca_step(render=fused)
-            if not fused:
-                env.render_observation(None)
         env.post_step(action, stats=True)
         if fused:
             call("gca_obs_position", env.obs_params, E, N, N, dev.ptr(env.pos), dev.ptr(env.is_night),
                  dev.ptr(env.time_step), dev.ptr(env.rgb), st)
+        else:
+            env.render_observation(None)
 
     dt_rgb, kern_rgb = timed_loop(step_rgb, args.steps, args.warmup, pg, device, reps=3, prepare=prep)
 
