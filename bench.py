@@ -918,6 +918,7 @@ def main():
             "env_steps_per_s": alex["env_steps_per_s"],
             "episode_start": alex.get("episode_start"),
             "with_rgb_observation": alex.get("with_rgb_observation"),
+            "with_rgb_observation_extensions": alex.get("with_rgb_observation_extensions"),
             # achieved = SURVEY.md §8d's algorithmic figure (41 B per cell-update, "independent of the build's
             # actual layout") x cells / the kernel's mean launch time; the bytes this build actually moves
             # (packed layout: 23.125 B/cell) and the PMC traffic are reported beside it

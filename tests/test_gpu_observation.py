@@ -120,10 +120,10 @@ def test_fused_step_observation_matches_reference(device, tile_skip):
     E, H, W = 3, 256, 512
     env = AdvancedForestFireBulldozerEnv(H, W, key=8, num_envs=E, use_hidden=True, device=device, observation="grid",
                                          hidden_rng="philox", tile_skip=tile_skip)
+    env.reset()
     # observation="rgb" needs a square grid for the reset frame; the step frame does not: give this env an RGB buffer
     env.rgb = torch.zeros((E, H, W, 3), dtype=torch.float32, device=device)
     assert env.fused_observation
-    env.reset()
     env.pos[:, 0], env.pos[:, 1] = 190, 60  # near the initial fire: shots land on burning / tree cells
     env.time_step.fill_(398)
     rng = np.random.default_rng(4)
