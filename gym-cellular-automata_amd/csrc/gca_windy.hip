@@ -278,11 +278,14 @@ __device__ __forceinline__ uint32_t wave_shl1(uint32_t v) {  // lane l <- lane l
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, true);
 }
 
+// S: the env's wave-uniform base (SGPRs), lofs: the lane's 32-bit column offset, R wave-uniform: the clamp and the row
+// offset stay scalar and the load is one global_load with an SGPR base and a 32-bit VGPR offset (no 64-bit address
+// VGPRs, no per-lane row arithmetic)
 template <int NW>
-__device__ __forceinline__ RowRaw<NW> load_rowraw(const uint8_t* __restrict__ S, int R, int H) {
+__device__ __forceinline__ RowRaw<NW> load_rowraw(const uint8_t* __restrict__ S, uint32_t lofs, int R, int H) {
     constexpr int W = 256 * NW;
     const int Rc = min(max(R, 0), H - 1);  // clamped: the value of an out-of-grid row is discarded by classify
-    const uint8_t* p = S + (int64_t)Rc * W;
+    const uint8_t* p = S + (uint32_t)Rc * (uint32_t)W + lofs;
     RowRaw<NW> x;
     if (NW == 1) {
         x.w[0] = *reinterpret_cast<const uint32_t*>(p);
@@ -326,23 +329,33 @@ __global__ __launch_bounds__(256) void windy_rows_kernel(uint8_t* __restrict__ b
     const int env = blockIdx.x / blocks_per_env;
     const int sblk = blockIdx.x - env * blocks_per_env;
     if (steps && steps[env] <= pass) return;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // the wave index is wave-uniform: readfirstlane keeps s0 and every row index in SGPRs
+    const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int s0 = (sblk * 4 + wave) * SH;
     if (s0 >= H) return;
     const bool odd = parity && parity[env];
     const int64_t HW = (int64_t)H * W;
-    const uint8_t* __restrict__ S = (odd ? buf1 : buf0) + (int64_t)env * HW + 4 * NW * lane;
-    uint8_t* __restrict__ Dst = (odd ? buf0 : buf1) + (int64_t)env * HW + 4 * NW * lane;
-    const uint32_t m = dir_mask[env];
-    const uint32_t m0 = (m & 1u) ? ~0u : 0u, m1 = (m & 2u) ? ~0u : 0u, m2 = (m & 4u) ? ~0u : 0u,
-                   m3 = (m & 8u) ? ~0u : 0u, m4 = (m & 16u) ? ~0u : 0u, m5 = (m & 32u) ? ~0u : 0u,
-                   m6 = (m & 64u) ? ~0u : 0u, m7 = (m & 128u) ? ~0u : 0u;
+    const uint8_t* __restrict__ S = (odd ? buf1 : buf0) + (int64_t)env * HW;
+    uint8_t* __restrict__ Dst = (odd ? buf0 : buf1) + (int64_t)env * HW;
+    const uint32_t lofs = 4 * NW * (uint32_t)lane;
+    // the env's direction mask, forced into an SGPR (a VGPR copy made hipcc rebuild some masks per row)
+    const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane((int)dir_mask[env]);
+    // all-ones / zero per direction, made opaque (readfirstlane) so that hipcc keeps `(x & m) | acc` as one
+    // v_and_or_b32 per direction instead of turning each mask into a v_cndmask plus a separate or
+    auto dm = [&](uint32_t bit) {
+        uint32_t v = (m & bit) ? ~0u : 0u;
+        asm volatile("" : "+s"(v));  // opaque SGPR value
+        return v;
+    };
+    const uint32_t m0 = dm(1u), m1 = dm(2u), m2 = dm(4u), m3 = dm(8u), m4 = dm(16u), m5 = dm(32u), m6 = dm(64u),
+                   m7 = dm(128u);
 
+    const uint32_t codes = (Ep & 0xFFu) | ((Tp & 0xFFu) << 8) | ((Fp & 0xFFu) << 16);
     // ring[k % RD] holds row s0 + 1 + k (k = 0 .. SH): the strip's rows below row s0 up to its lower halo row
     RowRaw<NW> ring[RD];
-    const RowRaw<NW> r_up = load_rowraw<NW>(S, s0 - 1, H), r_cur = load_rowraw<NW>(S, s0, H);
+    const RowRaw<NW> r_up = load_rowraw<NW>(S, lofs, s0 - 1, H), r_cur = load_rowraw<NW>(S, lofs, s0, H);
 #pragma unroll
-    for (int k = 0; k < RD; ++k) ring[k] = load_rowraw<NW>(S, s0 + 1 + k, H);
+    for (int k = 0; k < RD; ++k) ring[k] = load_rowraw<NW>(S, lofs, s0 + 1 + k, H);
     RowCls<NW> A = classify_row<NW>(r_up, s0 >= 1, Tp, Fp);
     RowCls<NW> B = classify_row<NW>(r_cur, true, Tp, Fp);
 
@@ -352,24 +365,32 @@ __global__ __launch_bounds__(256) void windy_rows_kernel(uint8_t* __restrict__ b
         const int Rc = s0 + t;
         // row Rc + 1: loaded RD rows ago; its slot is refilled with row Rc + 1 + RD right away
         const RowCls<NW> C = classify_row<NW>(ring[t % RD], Rc + 1 < H, Tp, Fp);
-        if (t + RD < SH) ring[t % RD] = load_rowraw<NW>(S, Rc + 1 + RD, H);
+        if (t + RD < SH) ring[t % RD] = load_rowraw<NW>(S, lofs, Rc + 1 + RD, H);
         uint32_t outw[NW];
         int32_t rowT = 0, rowF = 0;
 #pragma unroll
         for (int j = 0; j < NW; ++j) {
             // d -> source (r+1-a, c+1-b): d0 down/c+1, d1 down, d2 down/c-1, d3 cur/c+1, d4 cur/c-1, d5 up/c+1,
             // d6 up, d7 up/c-1 (as windy_fast_kernel)
-            const uint32_t any = (C.fr[j] & m0) | (C.f[j] & m1) | (C.fl[j] & m2) | (B.fr[j] & m3) | (B.fl[j] & m4) |
-                                 (A.fr[j] & m5) | (A.f[j] & m6) | (A.fl[j] & m7);
-            const uint32_t ign = B.t[j] & any;    // TREE -> FIRE
-            const uint32_t keep = B.t[j] & ~any;  // TREE stays
-            const uint32_t ignm = (ign << 8) - ign, keepm = (keep << 8) - keep;
-            outw[j] = (ignm & Fp) | (keepm & Tp) | (~(ignm | keepm) & Ep);
+            // any = OR_d (flags_d & m_d): one v_bitop3 (a & b) | c (table 0xEA) per direction
+            uint32_t any = C.fr[j] & m0;
+            any = __builtin_amdgcn_bitop3_b32(C.f[j], m1, any, 0xEA);
+            any = __builtin_amdgcn_bitop3_b32(C.fl[j], m2, any, 0xEA);
+            any = __builtin_amdgcn_bitop3_b32(B.fr[j], m3, any, 0xEA);
+            any = __builtin_amdgcn_bitop3_b32(B.fl[j], m4, any, 0xEA);
+            any = __builtin_amdgcn_bitop3_b32(A.fr[j], m5, any, 0xEA);
+            any = __builtin_amdgcn_bitop3_b32(A.f[j], m6, any, 0xEA);
+            any = __builtin_amdgcn_bitop3_b32(A.fl[j], m7, any, 0xEA);
+            const uint32_t ign = B.t[j] & any;  // TREE -> FIRE
+            const uint32_t keep = B.t[j] ^ ign;  // TREE stays
+            // output byte = code[2 ign + keep] (0 EMPTY, 1 TREE, 2 FIRE): one v_perm_b32 on the packed codes (hipcc
+            // turned the previous (x << 8) - x byte masks into quarter-rate v_mul_lo_u32)
+            outw[j] = __builtin_amdgcn_perm(codes, codes, (ign << 1) + keep);
             rowF += __popc(ign);
             rowT += __popc(keep);
         }
         if (Rc < H && t < SH) {
-            uint8_t* p = Dst + (int64_t)Rc * W;
+            uint8_t* p = Dst + (uint32_t)Rc * (uint32_t)W + lofs;
             if (NW == 1) *reinterpret_cast<uint32_t*>(p) = outw[0];
             else if (NW == 2) *reinterpret_cast<uint2*>(p) = make_uint2(outw[0], outw[1 % NW]);
             else *reinterpret_cast<uint4*>(p) = make_uint4(outw[0], outw[1 % NW], outw[2 % NW], outw[3 % NW]);
