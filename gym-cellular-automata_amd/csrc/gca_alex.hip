@@ -190,6 +190,23 @@ struct AlexObs {
     float* rgb;              // [E][H][W][3]
 };
 
+#ifdef GCA_ALEX_STAMPS  // A/B diagnostics build only: s_memtime at the phase boundaries of sampled PK workgroups
+constexpr int STAMP_SAMPLES = 4096, STAMP_N = 7;
+__device__ unsigned long long g_alex_stamps[STAMP_SAMPLES][4][STAMP_N];
+#define ALEX_STAMP(i)                                                                                   \
+    do {                                                                                                \
+        if (PK && stamp_slot >= 0) {                                                                     \
+            unsigned long long t_;                                                                      \
+            __builtin_amdgcn_sched_barrier(0);                                                          \
+            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");               \
+            __builtin_amdgcn_sched_barrier(0);                                                          \
+            if ((threadIdx.x & 63) == 0) g_alex_stamps[stamp_slot][threadIdx.x >> 6][i] = t_;          \
+        }                                                                                               \
+    } while (0)
+#else
+#define ALEX_STAMP(i) do {} while (0)
+#endif
+
 template <int R, int MODE, bool FAST, bool ES, bool PK = false, bool OBS = false>
 __global__ __launch_bounds__(NT, GCA_ALEX_WGS) void alex_step_kernel(
     gca_alex_params p, int H, int W, int tiles_r, int tiles_c, const uint8_t* __restrict__ grid_in,
@@ -224,6 +241,10 @@ __global__ __launch_bounds__(NT, GCA_ALEX_WGS) void alex_step_kernel(
     const int lb = (xcd < rn8 ? xcd * (qn8 + 1) : rn8 * (qn8 + 1) + (xcd - rn8) * qn8) + slot;
     const int e = lb / tiles;
     const int tile = lb - e * tiles;
+#ifdef GCA_ALEX_STAMPS
+    const int stamp_slot = (lb % 64 == 0 && lb / 64 < STAMP_SAMPLES) ? lb / 64 : -1;
+#endif
+    ALEX_STAMP(0);
     const int r0 = (tile / tiles_c) * TH, c0 = (tile % tiles_c) * TW;
     const int64_t HW = (int64_t)H * W;
     const uint8_t* gE = grid_in + (int64_t)e * HW;
@@ -578,6 +599,7 @@ __global__ __launch_bounds__(NT, GCA_ALEX_WGS) void alex_step_kernel(
         wg_need = __syncthreads_or(near_fire) != 0;
     else
         __syncthreads();
+    ALEX_STAMP(1);
     uint32_t treeB = 0u, emptyB = 0u;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -660,6 +682,7 @@ __global__ __launch_bounds__(NT, GCA_ALEX_WGS) void alex_step_kernel(
     }
     __syncthreads();
     if (GCA_ALEX_PRIO >= 4) __builtin_amdgcn_s_setprio(GCA_ALEX_PRIO == 4 ? 1 : 0);  // past the last barrier
+    ALEX_STAMP(2);
 
     __builtin_amdgcn_sched_barrier(0);
 
@@ -780,6 +803,7 @@ __global__ __launch_bounds__(NT, GCA_ALEX_WGS) void alex_step_kernel(
         }
     }
 
+    ALEX_STAMP(3);
     // ---- FIRE bits of rows r-1, r, r+1: bit j of nbw[a] <-> staged column cc0 - 1 + j (j = 0..17)
     uint32_t nbw[3];
     fire_rows(nbw);
@@ -967,6 +991,7 @@ __global__ __launch_bounds__(NT, GCA_ALEX_WGS) void alex_step_kernel(
     }
 
     if (GCA_ALEX_PRIO == 3) __builtin_amdgcn_s_setprio(0);
+    ALEX_STAMP(4);
     // ---- draws: burn / grow masks and the packed new-fire ages NA (two cells per word)
     uint32_t burn, grow, NA[8];
     if (INJECT) {
@@ -1067,6 +1092,7 @@ __global__ __launch_bounds__(NT, GCA_ALEX_WGS) void alex_step_kernel(
         nagew[pp] = bfi32(bm, NA[pp], a1);
     }
 
+    ALEX_STAMP(5);
     // ---------------- stores
     if (GCA_ALEX_PRIO == 2 || GCA_ALEX_PRIO == 3) __builtin_amdgcn_s_setprio(3);  // (A/B hook) finish and free the slot
     if (vec) {
@@ -1085,6 +1111,7 @@ __global__ __launch_bounds__(NT, GCA_ALEX_WGS) void alex_step_kernel(
         }
     }
     write_rgb(newT, newF);
+    ALEX_STAMP(6);
     if (counts || (PK && act_out)) {
         int cntT = __builtin_popcount(newT & okB), cntF = __builtin_popcount(newF & okB),
             cntE = __builtin_popcount(newE & okB);
@@ -1287,6 +1314,12 @@ extern "C" int gca_alex_step_packed_rgb(const gca_alex_params* p, int E, int H, 
                                  wind_index, rng_step, counts, act_in, act_out,
                                  AlexObs{reinterpret_cast<const float4*>(color_table), is_night, rgb}, stream);
 }
+
+#ifdef GCA_ALEX_STAMPS
+extern "C" int gca_debug_alex_stamps(unsigned long long* host_out) {
+    return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_alex_stamps), sizeof(g_alex_stamps)) == hipSuccess ? 0 : 2;
+}
+#endif
 
 // ------------------------------------------------------------------ packed env layers
 namespace {
