@@ -7,7 +7,8 @@ Alexandridis rule, E = 4096 envs per GPU, N = 256, use_hidden=False (veg = den =
 altitude 0 -> p_slope = 1, still read from HBM every step), mid-episode synthetic state
 (grid iid {EMPTY .1, TREE .8, FIRE .1}, fire ages iid [1, 672], wind_index iid [0, 8)),
 p_tree = 0, p_wind_change = 0.06. One timed step = random actions (device Philox) +
-the CA step (gca_alex_step_packed: packed edge-slope layout, 23.1 B/cell moved) + the env step (gca_advenv_post) [+ one RCCL all_gather of the
+the CA step (gca_alex_step_march at 256^2: packed edge-slope layout, 23.1 B/cell moved; gca_alex_step_packed
+with --step-kernel tiled) + the env step (gca_advenv_post) [+ one RCCL all_gather of the
 per-env done mask / reward when --gpus > 1]. Weak scaling: every rank owns E envs.
 
 Also reported: the WindyForestFire bulldozer env (config 2, E = 1024) as `secondary`,
@@ -30,7 +31,7 @@ for _p in (ROOT, os.path.join(ROOT, "gym-cellular-automata_amd")):
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # HBM bytes per Alexandridis cell-update this build moves: grid r+w 2, age r+w 4, veg 1, den 1,
 # dousing 1, + slopes: edge layout 4 x f32 = 16 (gca_alex_step_es), 8-plane p_slope 8 x f32 = 32;
-# packed env layout (gca_alex_step_packed): veg|den in one byte, dousing 1 bit, edge slopes 16
+# packed env layout (gca_alex_step_march / _packed): veg|den in one byte, dousing 1 bit, edge slopes 16
 ALEX_BYTES = {"packed": 23.125, "edge": 25, "planes": 41}
 ALEX_BYTES_PER_CELL = 41  # the SURVEY.md §8d figure (8-plane layout), reported alongside
 WINDY_BYTES_PER_CELL = 2  # u8 read + u8 write
@@ -53,6 +54,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--slope-layout", choices=["packed", "edge", "planes"], default="packed")
     ap.add_argument("--tile-skip", action="store_true", help="A/B: headline with the tile activity map on")
+    ap.add_argument("--step-kernel", choices=["auto", "march", "tiled"], default="auto",
+                    help="packed layout at W = 256: the marching kernel (auto) or the tiled one")
     ap.add_argument("--headline-only", action="store_true",
                     help="only the headline loop (no RGB / episode-start loops): every alex_step launch is the "
                          "dense mid-episode one, so rocprofv3 per-kernel averages match kernel_ms")
@@ -217,7 +220,8 @@ def bench_alex(args, world, rank, device, pg):
     E, N = args.envs, args.size
     env = AdvancedForestFireBulldozerEnv(N, N, key=1, num_envs=E, use_hidden=False, device=device,
                                          env_offset=rank * E, slope_layout=args.slope_layout, observation="rgb",
-                                         enable_extensions=False, tile_skip=args.tile_skip)
+                                         enable_extensions=False, tile_skip=args.tile_skip,
+                                         step_kernel=args.step_kernel if args.slope_layout == "packed" else "auto")
     env.reset()
     synthetic_state(env, rank, device)
     action = torch.zeros((E, 2), dtype=torch.int32, device=device)
@@ -255,11 +259,15 @@ def bench_alex(args, world, rank, device, pg):
         "survey_equiv_gbs": ALEX_BYTES_PER_CELL * E * N * N / kern / 1e9,
         "fires_left": int((env.counts[:, 2] > 0).sum().item()),
         "timing": detail,
+        "kernel": ("alex_march_kernel" if getattr(env, "march", False) else
+                   "alex_step_kernel" + {"packed": "<ES, PK>", "edge": "<ES>", "planes": ""}[args.slope_layout]),
     }
+    if getattr(env, "march", False) and rank == 0:
+        res["tiled_kernel_ms"] = tiled_kernel_ms(env, device)
     if args.headline_only:
         return res
     # the full reference env step: + the RGB observation of stateless_step (advanced_bulldozer.py:1120). The reference's
-    # default env (enable_extensions=False) gets it from the CA step's own epilogue (gca_alex_step_packed_rgb: 12 B/cell
+    # default env (enable_extensions=False) gets it from the CA step's own epilogue (gca_alex_step_march_rgb: 12 B/cell
     # of f32 RGB written, no second pass) + the bulldozer's pixel (gca_obs_position)
     fused = env.fused_observation  # the packed layout (the default); --slope-layout edge / planes: its own pass
 
@@ -814,6 +822,38 @@ def bench_dropins(device):
     return out
 
 
+def tiled_kernel_ms(env, device, K=10, reps=3):
+    """The same C3 state through the tiled packed kernel (gca_alex_step_packed, coalesced slopes) that the marching
+    kernel replaced at W = 256: mean launch time (HIP events, median of reps), for the record beside kernel_ms."""
+    import torch
+
+    from gymca_amd import _device as dev
+    from gymca_amd._lib import call
+
+    E, H, W = env.num_envs, env.nrows, env.ncols
+    st = dev.stream_ptr(device)
+    coal = torch.empty_like(env.slope_data)
+    call("gca_alex_edge_slope_coalesce", dev.ptr(env.slope_data), dev.ptr(coal), E, H, W, st)
+    times = []
+    for _ in range(reps):
+        synthetic_state(env, 0, device)
+        a0, b0 = env.cur, 1 - env.cur
+        for k in range(K + 1):
+            if k == 1:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+            a, b = (a0, b0) if k % 2 == 0 else (b0, a0)
+            call("gca_alex_step_packed", env.alex_params, E, H, W, dev.ptr(env.grid[a]), dev.ptr(env.grid[b]),
+                 dev.ptr(env.age[a]), dev.ptr(env.age[b]), dev.ptr(env.vd), dev.ptr(env.dous_bits), dev.ptr(coal),
+                 dev.ptr(env.wind_index), dev.ptr(env.rng_step), dev.ptr(env.counts), None, None, st)
+        e1.record()
+        torch.cuda.synchronize(device)
+        times.append(e0.elapsed_time(e1) / K)
+    del coal
+    synthetic_state(env, 0, device)
+    return sorted(times)[len(times) // 2]
+
+
 def measured_traffic(args):
     """HBM bytes per alex_step launch from the committed rocprofv3 PMC summary
     (profiles/pmc_traffic.json, written by scripts/pmc_summary.py: 2*FETCH_SIZE + WRITE_SIZE,
@@ -825,7 +865,8 @@ def measured_traffic(args):
         data = json.load(open(tf))
     except (ValueError, OSError):
         return None
-    want = {"packed": "alex_step<6, 0, true, true, true>", "edge": "alex_step<6, 0, true, true, false>",
+    want = {"packed": "alex_march<6, false>" if args.step_kernel != "tiled" else "alex_step<6, 0, true, true, true>",
+            "edge": "alex_step<6, 0, true, true, false>",
             "planes": "alex_step<6, 0, true, false, false>"}[args.slope_layout]
     for k, v in data.items():  # the Philox-mode FAST kernel at R = 6 (N = 256) of this slope layout
         if k == want:
@@ -924,8 +965,9 @@ def main():
             # (packed layout: 23.125 B/cell) and the PMC traffic are reported beside it
             "roofline": {"bound": "hbm", "achieved": alex["survey_equiv_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": alex["survey_equiv_gbs"] / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "alex_step_kernel" + {"packed": "<ES, PK>", "edge": "<ES>", "planes": ""}[args.slope_layout],
+                         "kernel": alex["kernel"],
                          "kernel_ms": alex["kernel_ms"],
+                         "tiled_kernel_ms": alex.get("tiled_kernel_ms"),
                          "algorithmic_bytes_per_cell": ALEX_BYTES_PER_CELL,
                          "slope_layout": args.slope_layout,
                          "moved_bytes_per_cell": ALEX_BYTES[args.slope_layout],

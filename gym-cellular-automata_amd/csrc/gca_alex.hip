@@ -24,7 +24,7 @@
 //        Philox = one Philox4x32-10 block per cell pair: words (main, aux) per cell;
 //        burn iff u(main) < 1 - prod_{fire d}(1 - clamp01(p_d)) (same law as independent draws),
 //        grow iff u(main) < p_tree, new fire age = randint(aux).
-#include "gca_common.h"
+#include "gca_alex_rule.h"
 
 namespace {
 
@@ -51,56 +51,22 @@ static_assert(CWP >= CW, "staged row fits");
 __host__ __device__ constexpr int pcol(int c) { return 16 * (c >> 4) + 4 * ((((c >> 2) & 3) + (c >> 6)) & 3) + (c & 3); }
 static_assert(CWP % 4 == 0, "16-B aligned rows");
 
-typedef float f2 __attribute__((ext_vector_type(2)));
+typedef gca_f2 f2;
 typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
 typedef int16_t i16x2 __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ float clamp01(float v) { return fminf(fmaxf(v, 0.0f), 1.0f); }
-// clamp01(a * b) on both halves: one v_pk_mul_f32 with the clamp output modifier; the product is
-// rounded first, then clamped (= clamp01(__fmul_rn(a, b)), NaN -> 0 like fminf(fmaxf(NaN, 0), 1))
-__device__ __forceinline__ f2 pk_mul_clamp01(f2 a, f2 b) {
-    f2 r;
-    asm("v_pk_mul_f32 %0, %1, %2 clamp" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
+__device__ __forceinline__ float clamp01(float v) { return gca_clamp01(v); }
+__device__ __forceinline__ f2 pk_mul_clamp01(f2 a, f2 b) { return gca_pk_mul_clamp01(a, b); }
 // bits = 2 * bits + (a < b): v_cmp into VCC + add-with-carry (cell 0 lands in the top bit; reversed later)
 __device__ __forceinline__ uint32_t push_lt(uint32_t bits, float a, float b) {
     asm("v_cmp_lt_f32 vcc, %1, %2\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc" : "+v"(bits) : "v"(a), "v"(b) : "vcc");
     return bits;
 }
-// 4-bit mask of the bytes of x equal to the byte of pat (bit j <-> byte j)
-__device__ __forceinline__ uint32_t eq_nib(uint32_t x, uint32_t pat) { return (bytes_eq01(x, pat) * 0x01020408u) >> 24; }
-// nibble (bit j) -> 0x01 in byte j; the four partial products never overlap
-__device__ __forceinline__ uint32_t spread4(uint32_t n) { return ((n & 0xFu) * 0x00204081u) & 0x01010101u; }
-__device__ __forceinline__ uint32_t bfi32(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
-// bit i of w as an all-ones / all-zeros word (v_bfe_i32)
-__device__ __forceinline__ uint32_t sbit(uint32_t w, int i) { return (uint32_t)((int32_t)(w << (31 - i)) >> 31); }
-
-// p_slope factors of a cell pair from edge-layout values V = +-exp_f32(|a|) (see ES below): own direction
-// (the edge's slope a): P(a) = V if V > 0 else 1/|V|; the neighbour's edge seen from the other end
-// (slope -a): P(-a) = |V| if V < 0 else 1/|V|. With rc = 1/V (signed: v_rcp_f32 + one packed Newton
-// step, the exact negation of the same steps on |V|) and |V| >= 1 >= |rc|, the selections are
-// P(a) = max(V, -rc) and P(-a) = max(-V, rc): one v_max_f32 per cell instead of a compare and a select.
-__device__ __forceinline__ f2 edge_factor_pair(float v0, float v1, bool own) {
-    const f2 x = {v0, v1};
-    const f2 r0 = {__builtin_amdgcn_rcpf(v0), __builtin_amdgcn_rcpf(v1)};
-    // ee = 1 - x * r0 on both halves (neg modifiers in the instruction; the compiler sometimes emits sign
-    // xors). The s_nop covers the v_rcp_f32 (trans) -> VALU read hazard, which the hazard recogniser does
-    // not apply to inline-asm operands (without it the high half read a stale r0).
-    f2 ee;
-    asm("s_nop 1\n\tv_pk_fma_f32 %0, %1, %2, 1.0 op_sel_hi:[1,1,0] neg_lo:[1,0,0] neg_hi:[1,0,0]"
-        : "=v"(ee) : "v"(x), "v"(r0));
-    const f2 rc = __builtin_elementwise_fma(ee, r0, r0);
-    f2 o;  // v_max_f32 with a neg source modifier (fmaxf would add canonicalising maxes and sign xors)
-    if (own) {
-        asm("v_max_f32_e64 %0, %1, -%2" : "=v"(o.x) : "v"(v0), "v"(rc.x));
-        asm("v_max_f32_e64 %0, %1, -%2" : "=v"(o.y) : "v"(v1), "v"(rc.y));
-    } else {
-        asm("v_max_f32_e64 %0, -%1, %2" : "=v"(o.x) : "v"(v0), "v"(rc.x));
-        asm("v_max_f32_e64 %0, -%1, %2" : "=v"(o.y) : "v"(v1), "v"(rc.y));
-    }
-    return o;
-}
+__device__ __forceinline__ uint32_t eq_nib(uint32_t x, uint32_t pat) { return gca_eq_nib(x, pat); }
+__device__ __forceinline__ uint32_t spread4(uint32_t n) { return gca_spread4(n); }
+__device__ __forceinline__ uint32_t bfi32(uint32_t m, uint32_t a, uint32_t b) { return gca_bfi32(m, a, b); }
+__device__ __forceinline__ uint32_t sbit(uint32_t w, int i) { return gca_sbit(w, i); }
+__device__ __forceinline__ f2 edge_factor_pair(float v0, float v1, bool own) { return gca_edge_factor_pair(v0, v1, own); }
 // DPP moves inside a 16-lane row (= one image row of a workgroup: lanes q = 0..15)
 __device__ __forceinline__ float dpp_from_next(float old, float src) {  // lane q <- lane q+1; lane 15 keeps old
     return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(src), 0x101, 0xF, 0xF, false));
@@ -585,13 +551,7 @@ __global__ __launch_bounds__(NT, GCA_ALEX_WGS) void alex_step_kernel(
         near_fire |= (bits != 0u && sr >= RS - 1 && sr <= RS + TH) ? 1 : 0;
     }
     for (int cc = tid; cc < CWP; cc += NT) CP[cc] = 0u;
-    if (tid < 16) {
-        const int v = tid & 7;
-        // selects on the (SGPR) kernel arguments only: no dynamic indexing into the argument struct
-        const float av = v <= 1 ? p.veg1p[1] : v == 2 ? p.veg1p[2] : v == 3 ? p.veg1p[3] : v == 4 ? p.veg1p[4] : p.veg1p[5];
-        const float ad = v <= 1 ? p.den1p[1] : v == 2 ? p.den1p[2] : v == 3 ? p.den1p[3] : v == 4 ? p.den1p[4] : p.den1p[5];
-        LUT[tid] = tid < 8 ? av : ad;
-    }
+    if (tid < 16) LUT[tid] = gca_alex_lut_entry(p, tid);
     // MODE 0: does any TREE cell of this workgroup (wg_need) / this wave (wave_need) have a burning
     // neighbour? The other modes evaluate every probability.
     bool wg_need = true;

@@ -1,0 +1,687 @@
+// gca_alex_march.hip — the Alexandridis CA step on the Advanced env's packed layout, marching form (W = 256).
+// Reference: PartiallyObservableForestFireJax._update_grid (ca_alexandridis_jax.py:321-424) with
+// _compute_burn_probability (:164-206): the rule, the f32 arithmetic in its order and the Philox draws of
+// alex_step_kernel's packed mode (gca_alex.hip), bit for bit; only the work mapping differs.
+//
+// Mapping: one wave = one activity-map tile = 16 rows x 256 columns of one env. Lane l owns columns 4l .. 4l+3 of
+// every row and the wave walks its tile top to bottom, one row per iteration, with every input of row r+1 in
+// flight while row r is computed. No LDS staging and no workgroup barrier (the tiled kernel spent 31 % of a wave's
+// life staging its halo and building the column prefix, profiles/r03i):
+//   fire ring   FIRE flags (0x01 bytes, one dword per row) of rows r-R-1 .. r+R;
+//   V_k         per column, the FIRE count of the 2k+1 rows around r: V_k += row r+k - row r-1-k per row;
+//   B_k         the (2k+1) x (2k+1) box sum = the (2k+1)-column window of V_k: v_dot4_u32_u8 of the lane's dword
+//               and its DPP neighbours (lanes l-2 .. l+2, wave_shr / wave_shl) against constant 0/1 byte masks;
+//   D_1, D_2    the same on the dousing flags (3 x 3 and 5 x 5 boxes, a ring of 6 rows);
+//   heat = sum_k dw_k * B_k, dous = (inner - border) * D_1 + border * D_2, fma-chained as in gca_alex.hip.
+// Edge slopes in the natural edge layout (E, 4, H, W) (gca_alex_edge_slope_from_altitude): row r+1's four planes
+// arrive while row r is computed; they are row r's 'down' factors (directions 5, 6, 7) and then row r+1's own, so
+// every slope byte is read once (the tiled kernel re-reads three planes of row r+1 through L2: 27.4 B/cell of
+// traffic against 23.1 algorithmic, profiles/pmc_traffic.json). Lane reads are 16 B / 4 B / 8 B at 16 / 4 / 8 B
+// strides: 1 KiB, 256 B, 512 B contiguous per wave instruction.
+// The edge halo of a 256-column segment is the grid's zero border (W = 256): lane 0's left and lane 63's right
+// DPP neighbours read 0 (EMPTY / no dousing), and the border cells' slope factors are 1.
+#include "gca_alex_rule.h"
+
+#include <type_traits>
+
+namespace {
+
+constexpr int MW = 256;  // grid width (one segment per row)
+constexpr int SH = 16;   // rows per wave = one tile of the activity map (gca.h: gca_alex_step_packed)
+
+struct MarchObs {
+    const float4* col;     // [2 nights][3 kinds][2 dousing] colours (gca_obs_color_table)
+    const int32_t* night;  // [E] pre-step is_night
+    float* rgb;            // [E][H][W][3]
+};
+
+// DPP across the whole wave (gfx9 wave_shr:1 / wave_shl:1); the lane without a source reads 0 (bound_ctrl: no
+// `old` operand to materialise, one v_mov_b32_dpp each)
+__device__ __forceinline__ uint32_t from_prev(uint32_t v) {  // lane l <- lane l-1
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x138, 0xF, 0xF, true);
+}
+__device__ __forceinline__ uint32_t from_next(uint32_t v) {  // lane l <- lane l+1
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x130, 0xF, 0xF, true);
+}
+
+// byte mask of dword o (lane l+o, o in -2..2) inside the window of radius k around the lane's column j
+__host__ __device__ constexpr uint32_t win_mask(int o, int j, int k) {
+    uint32_t m = 0;
+    for (int b = 0; b < 4; ++b) {
+        const int c = 4 * o + b - j;
+        if (c >= -k && c <= k) m |= 1u << (8 * b);
+    }
+    return m;
+}
+// B[j] = sum of the byte counts X over columns 4l+j-k .. 4l+j+k (k <= 8: lanes l-2 .. l+2)
+__device__ __forceinline__ void window4(uint32_t X, int k, uint32_t (&B)[4]) {
+    uint32_t n[5] = {0u, 0u, X, 0u, 0u};
+    if (k >= 1) {
+        n[1] = from_prev(X);
+        n[3] = from_next(X);
+    }
+    if (k >= 5) {
+        n[0] = from_prev(n[1]);
+        n[4] = from_next(n[3]);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        uint32_t acc = 0u;
+#pragma unroll
+        for (int o = -2; o <= 2; ++o) {
+            const uint32_t m = win_mask(o, j, k);
+            if (m) acc = __builtin_amdgcn_udot4(n[o + 2], m, acc, false);
+        }
+        B[j] = acc;
+    }
+}
+
+__device__ __forceinline__ float4 ldf4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+// *(T*)((char*)base + off): a wave-uniform base and a 32-bit lane byte offset (global_load ... v_off, s[base])
+#ifndef GCA_MARCH_SBASE
+#define GCA_MARCH_SBASE 0
+#endif
+#ifndef GCA_MARCH_OBS_MODE
+#define GCA_MARCH_OBS_MODE 0  // fused frame: 0 = through the wave's LDS row (1 KiB per store), 1 / 2 = per-lane 48 B (nt / plain)
+#endif
+template <class T, class B> __device__ __forceinline__ T ld_at(const B* base, uint32_t off) {
+    if (!GCA_MARCH_SBASE) return *reinterpret_cast<const T*>(reinterpret_cast<const unsigned char*>(base) + off);
+    // (A/B hook GCA_MARCH_SBASE) the base through readfirstlane (a no-op on an SGPR value): hipcc otherwise folds loop-invariant parts of the
+    // uniform base into 64-bit VGPR offsets (8 extra VGPR pairs and a v_lshl_add_u64 per load)
+    const uint64_t b = (uint64_t)(uintptr_t)base;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b), hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+    typedef const __attribute__((address_space(1))) unsigned char* gptr;  // global, not flat
+    const gptr sb = (gptr)(((uint64_t)hi << 32) | lo);
+    return *reinterpret_cast<const T*>((const unsigned char*)(sb + off));  // (address space inferred: global)
+}
+typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+typedef int16_t i16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ i16x2 bitcast_i16x2(uint32_t v) { return __builtin_bit_cast(i16x2, v); }
+__device__ __forceinline__ u16x2 bitcast_u16x2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
+template <class T> __device__ __forceinline__ uint32_t bitcast_u32(T v) { return __builtin_bit_cast(uint32_t, v); }
+
+template <int R, bool OBS>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void alex_march_kernel(
+    gca_alex_params p, int H, int nwaves, const uint8_t* __restrict__ grid_in, uint8_t* __restrict__ grid_out,
+    const int16_t* age_in, int16_t* age_out,  // no __restrict__: the env updates ages in place
+    const uint8_t* __restrict__ vd, const uint16_t* __restrict__ dbits, const float* __restrict__ es,
+    const int32_t* __restrict__ wind_index, const uint32_t* __restrict__ rng_step, int32_t* __restrict__ counts,
+    const uint8_t* __restrict__ act_in, uint8_t* __restrict__ act_out, MarchObs obs) {
+    constexpr int NF = 2 * R + 2;  // fire ring rows r-R-1 .. r+R
+    __shared__ float lut[4][16];
+    __shared__ float4 colw[4][8];
+    __shared__ float4 img[OBS ? 4 : 1][OBS ? 192 : 1];  // OBS: one RGB row (3 KiB) per wave
+    __shared__ uint32_t fring[4][2 * NF * 64];              // per wave: the fire ring, each row twice
+
+    // the wave index in SGPRs: everything derived from it (env, rows, base pointers, wind) stays scalar
+    const int tid = threadIdx.x, wl = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    // XCD-aware order (as gca_alex.hip): blocks b, b+8, ... share an XCD; give each XCD a contiguous block range
+    const int nb = (int)gridDim.x;
+    const int xcd = (int)blockIdx.x & 7, slot = (int)blockIdx.x >> 3;
+    const int qn8 = nb >> 3, rn8 = nb & 7;
+    const int lb = (xcd < rn8 ? xcd * (qn8 + 1) : rn8 * (qn8 + 1) + (xcd - rn8) * qn8) + slot;
+    const int wv = lb * 4 + wl;
+    if (wv >= nwaves) return;  // wave-uniform; no barrier follows
+    const int strips = H / SH;
+    const int e = wv / strips, s = wv - e * strips, s0 = s * SH;
+    const uint32_t HW = (uint32_t)H * MW;
+    const uint8_t* gE = grid_in + (size_t)e * HW;
+    uint8_t* gO = grid_out + (size_t)e * HW;
+    const int16_t* aE = age_in + (size_t)e * HW;
+    int16_t* aO = age_out + (size_t)e * HW;
+    const uint8_t* vE = vd + (size_t)e * HW;
+    const uint16_t* dE = dbits + (size_t)e * (HW >> 4);
+    const float* sE = es + (size_t)e * 4 * HW;
+    const uint32_t lc = 4u * (uint32_t)lane;  // column of the lane's cell 0 (= its grid byte offset in a row)
+    const uint32_t lane_a = 2u * lc, lane_s = 4u * lc, lane_d = 2u * (uint32_t)(lane >> 2);  // ages, slopes, dousing
+    const uint32_t Fp = rep4((uint32_t)p.fire), Ep = rep4((uint32_t)p.empty), Tp = rep4((uint32_t)p.tree);
+
+    if (lane < 16) lut[wl][lane] = gca_alex_lut_entry(p, lane);
+    if (OBS && lane < 6) colw[wl][lane] = obs.col[6 * (obs.night[e] != 0 ? 1 : 0) + lane];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+    auto graw = [&](int r) -> uint32_t {  // grid bytes of the lane's 4 cells in row r (0 = EMPTY outside)
+        return (r >= 0 && r < H) ? *reinterpret_cast<const uint32_t*>(gE + (uint32_t)r * MW + lc) : 0u;
+    };
+    auto draw_bits = [&](int r) -> uint32_t {  // the u16 of dousing bits holding the lane's 4 cells
+        return (r >= 0 && r < H) ? (uint32_t)dE[(uint32_t)r * (MW / 16) + (uint32_t)(lane >> 2)] : 0u;
+    };
+    auto dflags = [&](uint32_t w16) -> uint32_t { return gca_spread4(w16 >> (4 * (lane & 3))); };
+    // RGB row r of the lane's 4 cells (kinds from the new TREE / FIRE nibbles, pre-step dousing flags) through the
+    // wave's LDS row: 48 B per lane in, 3 x 1 KiB contiguous non-temporal stores out
+    auto write_rgb_row = [&](int r, uint32_t tB, uint32_t fB, uint32_t dfl) {
+        if constexpr (OBS && GCA_MARCH_OBS_MODE != 0) {  // (A/B hook) each lane stores its own 48 B: 3 x 16 B
+            typedef float f4t __attribute__((ext_vector_type(4)));
+            float c[12];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int kind = ((tB >> j) & 1u) ? 1 : (((fB >> j) & 1u) ? 2 : 0);
+                const float4 cl = colw[wl][2 * kind + (int)((dfl >> (8 * j)) & 1u)];
+                c[3 * j] = cl.x;
+                c[3 * j + 1] = cl.y;
+                c[3 * j + 2] = cl.z;
+            }
+            f4t* dst = reinterpret_cast<f4t*>(obs.rgb + ((size_t)e * H + r) * (MW * 3) + 12 * lane);
+#pragma unroll
+            for (int t = 0; t < 3; ++t) {
+                const f4t v = {c[4 * t], c[4 * t + 1], c[4 * t + 2], c[4 * t + 3]};
+                if (GCA_MARCH_OBS_MODE == 1)
+                    __builtin_nontemporal_store(v, dst + t);
+                else
+                    dst[t] = v;
+            }
+        } else if constexpr (OBS) {
+            // one cell at a time (a colour is 4 VGPRs): cell j's RGB at byte 48 * lane + 12 * j of the row image
+            float* im = reinterpret_cast<float*>(img[wl]) + 12 * lane;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int kind = ((tB >> j) & 1u) ? 1 : (((fB >> j) & 1u) ? 2 : 0);
+                const float4 cl = colw[wl][2 * kind + (int)((dfl >> (8 * j)) & 1u)];
+                im[3 * j] = cl.x;
+                im[3 * j + 1] = cl.y;
+                im[3 * j + 2] = cl.z;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            typedef float f4t __attribute__((ext_vector_type(4)));
+            float* row = obs.rgb + ((size_t)e * H + r) * (MW * 3);
+#pragma unroll
+            for (int t = 0; t < 3; ++t) {
+                const float4 v = img[wl][64 * t + lane];
+                __builtin_nontemporal_store((f4t){v.x, v.y, v.z, v.w}, reinterpret_cast<f4t*>(row + 4 * (64 * t + lane)));
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // this row's reads before the next row's writes
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+    };
+
+    // ---- tile activity map (see gca_alex_step_packed): no FIRE in this tile or the tiles above / below at the
+    //      step's input -> nothing in the tile can change; copy it (act_in only with p_tree == 0, host-checked)
+    if (act_out) {
+        if (act_in) {
+            const uint8_t* A = act_in + (size_t)e * strips;
+            const int anyf = A[s] | (s > 0 ? A[s - 1] : 0) | (s + 1 < strips ? A[s + 1] : 0);
+            if (!anyf) {
+                int cE = 0, cT = 0;
+#pragma unroll 4
+                for (int i = 0; i < SH; ++i) {
+                    const int r = s0 + i;
+                    const uint32_t o = (uint32_t)r * MW + lc;
+                    const uint32_t g = *reinterpret_cast<const uint32_t*>(gE + o);
+                    *reinterpret_cast<uint32_t*>(gO + o) = g;
+                    if (age_in != age_out) *reinterpret_cast<uint2*>(aO + o) = *reinterpret_cast<const uint2*>(aE + o);
+                    cE += __builtin_popcount(bytes_eq01(g, Ep));
+                    cT += __builtin_popcount(bytes_eq01(g, Tp));
+                    if (OBS) write_rgb_row(r, gca_eq_nib(g, Tp), 0u, dflags(draw_bits(r)));
+                }
+                if (lane == 0) act_out[(size_t)e * strips + s] = 0;
+                if (counts) {
+#pragma unroll
+                    for (int off = 32; off > 0; off >>= 1) {
+                        cE += __shfl_xor(cE, off);
+                        cT += __shfl_xor(cT, off);
+                    }
+                    if (lane == 0) {
+                        if (cE) atomicAdd(counts + 3 * e + 0, cE);
+                        if (cT) atomicAdd(counts + 3 * e + 1, cT);
+                    }
+                }
+                return;
+            }
+        }
+    }
+
+    // ---- fire ring in LDS: the FIRE flags (0x01 bytes) of rows r-R-1 .. r+R, one dword per lane and row, each row
+    //      stored twice (slots t and t + NF), so that the rows around r sit at fixed offsets from one base that moves
+    //      by one slot per row: immediate-offset ds_read_b32, no register rotation
+    uint32_t* FR = fring[wl];
+    auto ring_put = [&](int t, uint32_t v) {  // relative row t = row - (s0 - R - 1)
+        const int sl = t % NF;
+        FR[sl * 64 + lane] = v;
+        FR[(sl + NF) * 64 + lane] = v;
+    };
+#pragma unroll
+    for (int t = 0; t < NF - 1; ++t) ring_put(t, bytes_eq01(graw(s0 - R - 1 + t), Fp));
+    uint32_t dring[6];
+#pragma unroll
+    for (int t = 0; t < 5; ++t) dring[t] = dflags(draw_bits(s0 - 3 + t));
+    // loads of row s0 (and the slopes of rows s0, s0+1)
+    uint32_t nG = graw(s0 + R), nD = draw_bits(s0 + 2), nOwn = graw(s0);
+    uint32_t nVD = *reinterpret_cast<const uint32_t*>(vE + (size_t)s0 * MW + lc);
+    uint2 nAge = *reinterpret_cast<const uint2*>(aE + (size_t)s0 * MW + lc);
+    float4 sc[4], sn[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        sc[k] = ldf4(sE + (size_t)k * HW + (size_t)s0 * MW + lc);
+        sn[k] = ldf4(sE + (size_t)k * HW + (size_t)min(s0 + 1, H - 1) * MW + lc);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    uint32_t V[R + 1];
+#pragma unroll
+    for (int k = 1; k <= R; ++k) {
+        uint32_t v = 0u;
+#pragma unroll
+        for (int t = R - k; t <= R + k; ++t) v += FR[t * 64 + lane];
+        V[k] = v;
+    }
+    uint32_t Dv1 = dring[1] + dring[2] + dring[3];
+    uint32_t Dv2 = dring[0] + Dv1 + dring[4];
+
+    // border columns 0 and 255 (lanes 0 / 63, elements 0 / 3): slope factor 1 (the rows 0 / H-1: kill_row below)
+    const bool col_lo = lane == 0, col_hi = lane == 63;
+    // row s0's own factors of planes 0..2 (row r's directions 0..2 read prepared own factors; plane 3 stays raw)
+    auto prep_own = [&](float4& v) {
+        const gca_f2 a = gca_edge_factors_own(v.x, v.y), b = gca_edge_factors_own(v.z, v.w);
+        v = make_float4(col_lo ? 1.0f : a.x, a.y, b.x, col_hi ? 1.0f : b.y);
+    };
+#pragma unroll
+    for (int k = 0; k < 3; ++k) prep_own(sc[k]);
+
+    float wind[8];
+    {
+        const int widx = wind_index[e];
+#pragma unroll
+        for (int d = 0; d < 8; ++d) wind[d] = p.winds[widx][d < 4 ? d : d + 1];
+    }
+    const uint32_t step = rng_step ? rng_step[e] : 0u;
+    const uint32_t k0 = (uint32_t)p.seed, k1 = (uint32_t)(p.seed >> 32);
+    const uint32_t env_id = (uint32_t)(p.env_offset + e);
+    const float pt24 = __fmul_rn(p.p_tree, 16777216.0f);
+    const float w_in_minus_bd = __fsub_rn(p.dous_inner, p.dous_border);
+    const uint32_t codes = (p.empty & 0xFFu) | ((p.tree & 0xFFu) << 8) | ((p.fire & 0xFFu) << 16);
+    int cntE = 0, cntT = 0, cntF = 0;
+
+    // one row of the tile. SC: row r's planes (0..2 as prepared own factors, 3 raw); SN: row r+1's raw planes.
+    // After the row, SN holds row r+1's prepared planes and SC row r+2's raw planes (loaded once direction 4 has
+    // read SC): the caller swaps the roles.
+    auto row = [&](const int i, float4 (&SC)[4], float4 (&SN)[4]) {
+        const int r = s0 + i;
+        // ---- this row's inputs (loaded one row ago); issue row r+1's (rows clamped into the grid: the last row's
+        //      loads are unused, and unconditional loads keep the two rows of the loop body branch-free)
+        const uint32_t gnew = nG, dnew = nD, own = nOwn, vdw = nVD;
+        const uint2 agep = nAge;
+        {  // (wave-uniform row base pointers + a 32-bit lane byte offset: SGPR-based addressing, no 64-bit VALU math)
+            const int rg = r + 1 + R, rd = r + 3;
+            const size_t r1 = (size_t)min(r + 1, H - 1);
+            const uint32_t g = ld_at<uint32_t>(gE + (size_t)min(rg, H - 1) * MW, lc);
+            const uint32_t d = ld_at<uint16_t>(dE + (size_t)min(rd, H - 1) * (MW / 16), lane_d);
+            nG = rg < H ? g : 0u;
+            nD = rd < H ? d : 0u;
+            nOwn = ld_at<uint32_t>(gE + r1 * MW, lc);
+            nVD = ld_at<uint32_t>(vE + r1 * MW, lc);
+            nAge = ld_at<uint2>(aE + r1 * MW, lane_a);
+        }
+        auto load_next_slopes = [&]() {  // row r+2's raw planes into SC
+            const size_t rs = (size_t)min(r + 2, H - 1);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) SC[k] = ld_at<float4>(sE + (size_t)k * HW + rs * MW, lane_s);
+        };
+        // ---- fire ring: row r+R enters; the running vertical sums move to row r
+        const int t0 = i % NF;  // slot of row r-R-1
+        uint32_t* Fb = FR + t0 * 64;
+        {
+            const uint32_t fnew = bytes_eq01(gnew, Fp);
+            Fb[(NF - 1) * 64 + lane] = fnew;
+            Fb[(t0 == 0 ? 2 * NF - 1 : -1) * 64 + lane] = fnew;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        uint32_t fm1, f0, fp1;  // FIRE flags of rows r-1, r, r+1
+        {
+            uint32_t rw[NF];
+#pragma unroll
+            for (int t = 0; t < NF; ++t) rw[t] = Fb[t * 64 + lane];
+#pragma unroll
+            for (int k = 1; k <= R; ++k) V[k] += rw[R + 1 + k] - rw[R - k];
+            fm1 = rw[R];
+            f0 = rw[R + 1];
+            fp1 = rw[R + 2];
+        }
+        dring[5] = dflags(dnew);
+        Dv1 += dring[4] - dring[1];
+        Dv2 += dring[5] - dring[0];
+
+        // ---- masks of the row: own kinds, FIRE neighbourhood (3 rows x 6 columns per lane)
+        const uint32_t treeB = gca_eq_nib(own, Tp), emptyB = gca_eq_nib(own, Ep);
+        const uint32_t nib3 = ((fm1 * 0x01020408u) >> 24) | (((f0 * 0x01020408u) >> 24) << 8) |
+                              (((fp1 * 0x01020408u) >> 24) << 16);
+        const uint32_t fireB = (nib3 >> 8) & 0xFu;
+        const uint32_t ext = ((from_prev(nib3) >> 3) & 0x010101u) | ((nib3 & 0x0F0F0Fu) << 1) |
+                             ((from_next(nib3) & 0x010101u) << 5);
+        auto dir_shift = [](int d) -> int {  // bit of ext holding direction d of the lane's cell 0
+            const int a = d < 3 ? 0 : (d < 5 ? 1 : 2);
+            const int b = d < 3 ? d : (d == 3 ? 0 : (d == 4 ? 2 : d - 5));
+            return 8 * a + b;
+        };
+        uint32_t anyfire = 0u;
+#pragma unroll
+        for (int d = 0; d < 8; ++d) anyfire |= ext >> dir_shift(d);
+        anyfire &= 0xFu;
+
+        gca_f2 qn[2] = {{1.0f, 1.0f}, {1.0f, 1.0f}};
+        const bool row_need = __ballot((treeB & anyfire) != 0u) != 0ull;
+        const bool kill_row = r == 0 || r == H - 1;       // every factor of row r is 1
+        const bool kill_next = r + 1 == H - 1;            // row r+1's own factors are 1 (prepared here)
+        // own factors of SN's plane k for row r+1 (and, when `nb`, the neighbour factors row r's directions 5..7 use)
+        auto prep_next = [&](int k, bool want_nb, float (&nbv)[4]) {
+            gca_f2 oa, ob, na, nb2;
+            if (want_nb) {
+                gca_edge_factors_both(SN[k].x, SN[k].y, oa, na);
+                gca_edge_factors_both(SN[k].z, SN[k].w, ob, nb2);
+                nbv[0] = na.x; nbv[1] = na.y; nbv[2] = nb2.x; nbv[3] = nb2.y;
+            } else {
+                oa = gca_edge_factors_own(SN[k].x, SN[k].y);
+                ob = gca_edge_factors_own(SN[k].z, SN[k].w);
+            }
+            SN[k] = make_float4(col_lo ? 1.0f : oa.x, oa.y, ob.x, col_hi ? 1.0f : ob.y);
+        };
+        if (!row_need) {
+            load_next_slopes();
+            float unused[4];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) prep_next(k, false, unused);
+        } else {
+            // ---- heat = heat0 + sum_k dw_k * B_k (k = 0..R, fma chain), minus the dousing term
+            gca_f2 ph[2] = {{p.heat0, p.heat0}, {p.heat0, p.heat0}};
+#pragma unroll
+            for (int k = 0; k <= R; ++k) {
+                uint32_t B[4];
+                if (k == 0) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) B[j] = (f0 >> (8 * j)) & 0xFFu;
+                } else {
+                    window4(V[k], k, B);
+                }
+                const float wk = p.heat_dw[k];
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+                    ph[h] = __builtin_elementwise_fma((gca_f2){wk, wk}, (gca_f2){(float)B[2 * h], (float)B[2 * h + 1]}, ph[h]);
+                // one radius at a time (hipcc would otherwise interleave all the radii's DPP / dot4 work)
+                asm volatile("" : "+v"(ph[0]), "+v"(ph[1]));
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            uint32_t D1[4], D2[4];
+            window4(Dv1, 1, D1);
+            window4(Dv2, 2, D2);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                gca_f2 dz = (gca_f2){w_in_minus_bd, w_in_minus_bd} * (gca_f2){(float)D1[2 * h], (float)D1[2 * h + 1]};
+                dz = __builtin_elementwise_fma((gca_f2){p.dous_border, p.dous_border},
+                                               (gca_f2){(float)D2[2 * h], (float)D2[2 * h + 1]}, dz);
+                ph[h] = ph[h] - dz;
+            }
+            // ---- base = (p_h * (1 + p_veg)) * (1 + p_den)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const uint32_t b0 = (vdw >> (16 * h)) & 0xFFu, b1 = (vdw >> (16 * h + 8)) & 0xFFu;
+                const gca_f2 av = {lut[wl][b0 & 7u], lut[wl][b1 & 7u]};
+                const gca_f2 ad = {lut[wl][8 + (b0 >> 4)], lut[wl][8 + (b1 >> 4)]};
+                ph[h] = (ph[h] * av) * ad;
+            }
+            // ---- directions, in order: qn = prod over burning d of (1 - clamp01(base * wind[d] * p_slope[d]));
+            //      rows 0 and H-1 (KILL: every factor 1, no edge arithmetic) take their own copy of the pass
+            auto dir_pass = [&](auto kill_tag) {
+                constexpr bool KILL = decltype(kill_tag)::value;
+                auto apply = [&](int d, const float (&a)[4]) {
+                    // pin base and the product: otherwise the direction-independent work of all 8 directions is
+                    // hoisted (as in gca_alex.hip)
+                    asm volatile("" : "+v"(ph[0]), "+v"(ph[1]), "+v"(qn[0]), "+v"(qn[1]));
+                    const int sh = dir_shift(d);
+                    const gca_f2 wd2 = {wind[d], wind[d]};
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const gca_f2 t = ph[h] * wd2;
+                        const gca_f2 c = KILL ? (gca_f2){gca_clamp01(t.x), gca_clamp01(t.y)}
+                                              : gca_pk_mul_clamp01(t, (gca_f2){a[2 * h], a[2 * h + 1]});
+                        const gca_f2 x = (gca_f2){1.0f, 1.0f} - c;
+                        const uint32_t x0 = gca_bfi32(gca_sbit(ext, sh + 2 * h), __float_as_uint(x.x), 0x3F800000u);
+                        const uint32_t x1 = gca_bfi32(gca_sbit(ext, sh + 2 * h + 1), __float_as_uint(x.y), 0x3F800000u);
+                        qn[h] = qn[h] * (gca_f2){__uint_as_float(x0), __uint_as_float(x1)};
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                };
+                const float one[4] = {1.0f, 1.0f, 1.0f, 1.0f};
+#pragma unroll
+                for (int d = 0; d < 3; ++d) {  // prepared own factors of planes 0..2
+                    const float a[4] = {SC[d].x, SC[d].y, SC[d].z, SC[d].w};
+                    apply(d, KILL ? one : a);
+                }
+                if (KILL) {
+                    apply(3, one);
+                    apply(4, one);
+                } else {  // plane 3 of row r: own factor (d = 3) and, one column on, the neighbour factor (d = 4)
+                    gca_f2 oa, ob, na, nb2;
+                    gca_edge_factors_both(SC[3].x, SC[3].y, oa, na);
+                    gca_edge_factors_both(SC[3].z, SC[3].w, ob, nb2);
+                    const float a3[4] = {col_lo ? 1.0f : oa.x, oa.y, ob.x, col_hi ? 1.0f : ob.y};
+                    apply(3, a3);
+                    // (r, c+1)'s plane 3; lane 63's last cell is column 255 (DPP old = 1.0)
+                    const float nx = __uint_as_float((uint32_t)__builtin_amdgcn_update_dpp(
+                        (int)0x3F800000u, (int)__float_as_uint(na.x), 0x130, 0xF, 0xF, false));
+                    const float a4[4] = {col_lo ? 1.0f : na.y, nb2.x, nb2.y, nx};
+                    apply(4, a4);
+                }
+                load_next_slopes();
+                float nb[4];
+                // plane 2 of (r+1, c-1): lane 0's first cell is column 0 (DPP old = 1.0)
+                prep_next(2, !KILL, nb);
+                if (KILL) {
+                    apply(5, one);
+                } else {
+                    const float pv = __uint_as_float((uint32_t)__builtin_amdgcn_update_dpp(
+                        (int)0x3F800000u, (int)__float_as_uint(nb[3]), 0x138, 0xF, 0xF, false));
+                    const float a5[4] = {pv, nb[0], nb[1], col_hi ? 1.0f : nb[2]};
+                    apply(5, a5);
+                }
+                // plane 1 of (r+1, c)
+                prep_next(1, !KILL, nb);
+                if (KILL) {
+                    apply(6, one);
+                } else {
+                    const float a6[4] = {col_lo ? 1.0f : nb[0], nb[1], nb[2], col_hi ? 1.0f : nb[3]};
+                    apply(6, a6);
+                }
+                // plane 0 of (r+1, c+1): lane 63's last cell is column 255 (DPP old = 1.0)
+                prep_next(0, !KILL, nb);
+                if (KILL) {
+                    apply(7, one);
+                } else {
+                    const float nx = __uint_as_float((uint32_t)__builtin_amdgcn_update_dpp(
+                        (int)0x3F800000u, (int)__float_as_uint(nb[0]), 0x130, 0xF, 0xF, false));
+                    const float a7[4] = {col_lo ? 1.0f : nb[1], nb[2], nb[3], nx};
+                    apply(7, a7);
+                }
+            };
+            if (kill_row)
+                dir_pass(std::true_type{});
+            else
+                dir_pass(std::false_type{});
+        }
+        if (kill_next) {  // row H-1: its own factors are 1 (its neighbour factors come from outside the grid)
+#pragma unroll
+            for (int k = 0; k < 3; ++k) SN[k] = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
+        }
+
+        // ---- draws: one Philox block per cell pair (cells 4l, 4l+1 and 4l+2, 4l+3), as gca_alex.hip
+        const uint32_t needB = (treeB & anyfire) | (p.p_tree > 0.0f ? emptyB : 0u);
+        const uint32_t lin0 = (uint32_t)r * MW + lc;
+        uint32_t burn = 0u, grow = 0u, NA[2];
+        // every lane draws when any lane of the wave needs to (a wave-uniform branch instead of a masked one per
+        // pair): the draws of cells that need none are discarded (qn = 1 gives thr = 0; grow is masked by EMPTY)
+        const bool wave_draws = __ballot(needB != 0u) != 0ull;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            u32x4 X = u32x4{0u, 0u, 0u, 0u};
+            if (wave_draws)
+                X = philox4x32_10(u32x4{(lin0 >> 1) + (uint32_t)h, env_id, step, GCA_TAG_ALEX_CELL}, k0, k1);
+            // thr = fl(1 - qn) * 2^24 = fl(2^24 - qn * 2^24) (power-of-two scaling commutes with the rounding)
+            const gca_f2 thr = __builtin_elementwise_fma(qn[h], (gca_f2){-16777216.0f, -16777216.0f},
+                                                         (gca_f2){16777216.0f, 16777216.0f});
+            const float u0 = (float)(X.x >> 8), u1 = (float)(X.z >> 8);
+            burn |= (u0 < thr.x ? 1u : 0u) << (2 * h);
+            burn |= (u1 < thr.y ? 1u : 0u) << (2 * h + 1);
+            grow |= (u0 < pt24 ? 1u : 0u) << (2 * h);
+            grow |= (u1 < pt24 ? 1u : 0u) << (2 * h + 1);
+            const uint32_t n0 = (uint32_t)randint_ms(X.y, p.age_lo, p.age_hi);
+            const uint32_t n1 = (uint32_t)randint_ms(X.w, p.age_lo, p.age_hi);
+            NA[h] = __builtin_amdgcn_perm(n1, n0, 0x05040100u);
+        }
+        burn &= treeB;
+        grow &= emptyB;
+
+        // ---- the rule on 4-bit masks: TREE -> FIRE (burn), EMPTY -> TREE (grow), FIRE -> EMPTY (age <= 1;
+        //      classic: age == 1); age <= 1 <=> sat(age - 2) < 0 (saturating i16 pairs, exact for every int16)
+        const uint32_t agw[2] = {agep.x, agep.y};
+        uint32_t le1;
+        if (!p.burnout_eq1) {
+            const uint32_t y0 = bitcast_u32(__builtin_elementwise_sub_sat(bitcast_i16x2(agw[0]), (i16x2){2, 2}));
+            const uint32_t y1 = bitcast_u32(__builtin_elementwise_sub_sat(bitcast_i16x2(agw[1]), (i16x2){2, 2}));
+            le1 = ((y0 >> 15) & 1u) | ((y0 >> 30) & 2u) | ((y1 >> 13) & 4u) | ((y1 >> 28) & 8u);
+        } else {
+            le1 = 0u;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                le1 |= ((int32_t)(int16_t)(agw[j >> 1] >> (16 * (j & 1))) == 1) ? (1u << j) : 0u;
+        }
+        const uint32_t newF = burn | (fireB & ~le1);
+        const uint32_t newT = (treeB & ~burn) | grow;
+        const uint32_t newE = (emptyB & ~grow) | (fireB & le1);
+        const uint32_t keepB = ~(treeB | emptyB | fireB) & 0xFu;  // codes outside {empty, tree, fire}: unchanged
+        uint32_t sel = gca_spread4(newT) + 2u * gca_spread4(newF);
+        sel |= (gca_spread4(keepB) * 0xFFu) & 0x07060504u;
+        const uint32_t outw = __builtin_amdgcn_perm(own, codes, sel);
+        // ages: FIRE cells age - 1 (also when they burn out), new fires the drawn age, others unchanged
+        uint32_t nag[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t fh = ((fireB >> (2 * h)) & 1u) | (((fireB >> (2 * h + 1)) & 1u) << 16);
+            const uint32_t a1 = bitcast_u32(bitcast_u16x2(agw[h]) - bitcast_u16x2(fh));
+            const uint32_t bm = (((burn >> (2 * h)) & 1u) * 0xFFFFu) | (((burn >> (2 * h + 1)) & 1u) * 0xFFFF0000u);
+            nag[h] = gca_bfi32(bm, NA[h], a1);
+        }
+        const size_t o = (size_t)r * MW + lc;
+        *reinterpret_cast<uint32_t*>(gO + o) = outw;
+        *reinterpret_cast<uint2*>(aO + o) = make_uint2(nag[0], nag[1]);
+        write_rgb_row(r, newT, newF, dring[3]);
+        cntT += __builtin_popcount(newT);
+        cntF += __builtin_popcount(newF);
+        cntE += __builtin_popcount(newE);
+
+#pragma unroll
+        for (int t = 0; t < 5; ++t) dring[t] = dring[t + 1];
+    };
+#pragma unroll 1
+    for (int i = 0; i < SH; i += 2) {
+        row(i, sc, sn);
+        row(i + 1, sn, sc);
+    }
+
+    if (counts || act_out) {
+        const bool anyF = __ballot(cntF != 0) != 0ull;
+        if (act_out && lane == 0) act_out[(size_t)e * strips + s] = anyF ? 1 : 0;
+        if (counts) {
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) {
+                cntT += __shfl_xor(cntT, off);
+                cntF += __shfl_xor(cntF, off);
+                cntE += __shfl_xor(cntE, off);
+            }
+            if (lane == 0) {
+                if (cntE) atomicAdd(counts + 3 * e + 0, cntE);
+                if (cntT) atomicAdd(counts + 3 * e + 1, cntT);
+                if (cntF) atomicAdd(counts + 3 * e + 2, cntF);
+            }
+        }
+    }
+}
+
+template <int R, bool OBS>
+void launch_march(const gca_alex_params& p, int E, int H, const uint8_t* gi, uint8_t* go, const int16_t* ai,
+                  int16_t* ao, const uint8_t* vd, const uint16_t* db, const float* es, const int32_t* wi,
+                  const uint32_t* rs, int32_t* counts, const uint8_t* act_in, uint8_t* act_out, MarchObs obs,
+                  hipStream_t st) {
+    const int nwaves = E * (H / SH);
+    hipLaunchKernelGGL((alex_march_kernel<R, OBS>), dim3((unsigned)((nwaves + 3) / 4)), dim3(256), 0, st, p, H, nwaves,
+                       gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs);
+}
+
+template <bool OBS>
+void dispatch_march(const gca_alex_params& p, int E, int H, const uint8_t* gi, uint8_t* go, const int16_t* ai,
+                    int16_t* ao, const uint8_t* vd, const uint16_t* db, const float* es, const int32_t* wi,
+                    const uint32_t* rs, int32_t* counts, const uint8_t* act_in, uint8_t* act_out, MarchObs obs,
+                    hipStream_t st) {
+#define GCA_MARCH_CASE(RV) \
+    case RV: launch_march<RV, OBS>(p, E, H, gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs, st); break;
+    switch (p.R) {
+#ifdef GCA_ALEX_ONLY_R
+        GCA_MARCH_CASE(GCA_ALEX_ONLY_R)
+#else
+        GCA_MARCH_CASE(1) GCA_MARCH_CASE(2) GCA_MARCH_CASE(3) GCA_MARCH_CASE(4)
+        GCA_MARCH_CASE(5) GCA_MARCH_CASE(6) GCA_MARCH_CASE(7) GCA_MARCH_CASE(8)
+#endif
+    }
+#undef GCA_MARCH_CASE
+}
+
+int march_impl(const gca_alex_params* p, int E, int H, int W, const uint8_t* grid_in, uint8_t* grid_out,
+               const int16_t* age_in, int16_t* age_out, const uint8_t* vd, const uint16_t* dous_bits,
+               const float* edge_slope, const int32_t* wind_index, const uint32_t* rng_step, int32_t* counts,
+               const uint8_t* act_in, uint8_t* act_out, MarchObs obs, void* stream) {
+    GCA_CHECK_ARG(p && grid_in && grid_out && age_in && age_out && vd && dous_bits && edge_slope && wind_index,
+                  "alex_step_march: null argument");
+    GCA_CHECK_ARG(E > 0 && H > 0 && W == MW && H % SH == 0, "alex_step_march: W must be 256 and H a multiple of 16");
+    GCA_CHECK_ARG(p->R >= 1 && p->R <= GCA_MAX_RADIUS, "alex_step_march: burn radius must be in [1, 8]");
+    GCA_CHECK_ARG(p->n_winds >= 1 && p->n_winds <= 16, "alex_step_march: 1..16 wind matrices");
+    GCA_CHECK_ARG((int64_t)E * (H / SH) < (int64_t)1 << 31, "alex_step_march: too many tiles");
+    GCA_CHECK_ARG(grid_in != grid_out, "alex_step_march: the grid cannot be updated in place");
+    GCA_CHECK_ARG(((((uintptr_t)grid_in) | ((uintptr_t)grid_out) | ((uintptr_t)age_in) | ((uintptr_t)age_out) |
+                    ((uintptr_t)vd) | ((uintptr_t)edge_slope) | ((uintptr_t)obs.rgb) | ((uintptr_t)obs.col)) & 15u) == 0 &&
+                      ((uintptr_t)dous_bits & 1u) == 0,
+                  "alex_step_march: arrays must be 16-B aligned");
+    GCA_CHECK_ARG(!act_in || act_out, "alex_step_march: act_in needs act_out");
+    GCA_CHECK_ARG(act_in != act_out || !act_in, "alex_step_march: act_in and act_out must differ");
+    hipStream_t st = (hipStream_t)stream;
+    if (counts && hipMemsetAsync(counts, 0, sizeof(int32_t) * 3 * (size_t)E, st) != hipSuccess) {
+        gca_set_error("alex_step_march: counts memset failed");
+        return GCA_ERR_HIP;
+    }
+    const uint8_t* ain = (p->p_tree > 0.0f) ? nullptr : act_in;  // growth can change a fire-free tile
+    if (obs.rgb)
+        dispatch_march<true>(*p, E, H, grid_in, grid_out, age_in, age_out, vd, dous_bits, edge_slope, wind_index,
+                             rng_step, counts, ain, act_out, obs, st);
+    else
+        dispatch_march<false>(*p, E, H, grid_in, grid_out, age_in, age_out, vd, dous_bits, edge_slope, wind_index,
+                              rng_step, counts, ain, act_out, obs, st);
+    GCA_CHECK_LAUNCH(obs.rgb ? "alex_step_march_rgb" : "alex_step_march");
+    return GCA_OK;
+}
+
+}  // namespace
+
+extern "C" int gca_alex_step_march(const gca_alex_params* p, int E, int H, int W, const uint8_t* grid_in,
+                                   uint8_t* grid_out, const int16_t* age_in, int16_t* age_out, const uint8_t* vd,
+                                   const uint16_t* dous_bits, const float* edge_slope, const int32_t* wind_index,
+                                   const uint32_t* rng_step, int32_t* counts, const uint8_t* act_in, uint8_t* act_out,
+                                   void* stream) {
+    return march_impl(p, E, H, W, grid_in, grid_out, age_in, age_out, vd, dous_bits, edge_slope, wind_index, rng_step,
+                      counts, act_in, act_out, MarchObs{nullptr, nullptr, nullptr}, stream);
+}
+
+extern "C" int gca_alex_step_march_rgb(const gca_alex_params* p, int E, int H, int W, const uint8_t* grid_in,
+                                       uint8_t* grid_out, const int16_t* age_in, int16_t* age_out, const uint8_t* vd,
+                                       const uint16_t* dous_bits, const float* edge_slope, const int32_t* wind_index,
+                                       const uint32_t* rng_step, int32_t* counts, const uint8_t* act_in,
+                                       uint8_t* act_out, const float* color_table, const int32_t* is_night, float* rgb,
+                                       void* stream) {
+    GCA_CHECK_ARG(color_table && is_night && rgb, "alex_step_march_rgb: color_table, is_night and rgb required");
+    return march_impl(p, E, H, W, grid_in, grid_out, age_in, age_out, vd, dous_bits, edge_slope, wind_index, rng_step,
+                      counts, act_in, act_out,
+                      MarchObs{reinterpret_cast<const float4*>(color_table), is_night, rgb}, stream);
+}

@@ -195,6 +195,9 @@ _SIGNATURES = {
     "gca_alex_step_packed": ([POINTER(AlexParams), c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, P, P, P], c_int),
     "gca_alex_step_packed_rgb": ([POINTER(AlexParams), c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, P, P, P, P,
                                   P, P], c_int),
+    "gca_alex_step_march": ([POINTER(AlexParams), c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, P, P, P], c_int),
+    "gca_alex_step_march_rgb": ([POINTER(AlexParams), c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, P, P, P, P,
+                                 P, P], c_int),
     "gca_obs_color_table": ([POINTER(ObsParams), P, P], c_int),
     "gca_obs_position": ([POINTER(ObsParams), c_int, c_int, c_int, P, P, P, P, P], c_int),
     "gca_alex_pack_layers": ([P, P, P, P, P, c_int, c_int, c_int, P], c_int),

@@ -33,8 +33,11 @@ derives the other 4 directions and exp in-kernel: gca_alex_step_es), plus per-en
 scalars: 25 B of HBM traffic per cell-update. slope_layout="packed" (the default
 "auto" when W % 256 == 0 and H % 16 == 0) runs gca_alex_step_packed on the same state with
 vegetation|density in one byte, the 0/1 dousing counts as bits and the edge slopes in coalesced
-segment order (23.1 B per cell-update; the u8 layers stay the API's context). slope_layout="planes"
-keeps the general 8-plane p_slope f32 [8][H][W] = exp(0.078*slope) (41 B per cell-update).
+segment order (23.1 B per cell-update; the u8 layers stay the API's context). At W = 256 the packed
+layout's step is the marching kernel (gca_alex_step_march: one wave walks a 16 x 256 tile row by row,
+the edge slopes in natural column order); step_kernel="tiled" keeps gca_alex_step_packed there.
+slope_layout="planes" keeps the general 8-plane p_slope f32 [8][H][W] = exp(0.078*slope) (41 B per
+cell-update).
 """
 import numpy as np
 
@@ -51,7 +54,8 @@ class AdvancedForestFireBulldozerEnv:
     def __init__(self, nrows, ncols, key=0, num_envs=8, speed_move=0.12, speed_act=0.03, speed_multiplier=1.0,
                  pos_bull=None, pos_fire=None, t_move=None, t_shoot=None, t_any=0.001, p_tree=0.90, p_empty=0.10,
                  use_hidden=True, middle_fire=False, enable_extensions=False, device=None, env_offset=0,
-                 hidden_rng=None, slope_layout="auto", observation="rgb", pinecones=False, tile_skip=False):
+                 hidden_rng=None, slope_layout="auto", observation="rgb", pinecones=False, tile_skip=False,
+                 step_kernel="auto"):
         import torch
 
         self.device = dev.require_device(device)
@@ -110,6 +114,11 @@ class AdvancedForestFireBulldozerEnv:
         if slope_layout == "packed" and (W % 256 or H % 16):
             raise ValueError("slope_layout='packed' needs W % 256 == 0 and H % 16 == 0")
         self.slope_layout = slope_layout
+        if step_kernel not in ("auto", "march", "tiled"):
+            raise ValueError("step_kernel must be 'auto', 'march' or 'tiled'")
+        if step_kernel == "march" and (slope_layout != "packed" or W != 256):
+            raise ValueError("step_kernel='march' needs the packed layout at W = 256")
+        self._step_kernel = step_kernel
         if slope_layout == "packed":  # the packed step updates ages in place: both "buffers" are one (stride 0)
             self.age = torch.zeros((E, H, W), dtype=torch.int16, **kw).unsqueeze(0).expand(2, E, H, W)
         # edge: (E, 4, H, W) edge values for gca_alex_step_es (packed: the same in coalesced order);
@@ -218,10 +227,15 @@ class AdvancedForestFireBulldozerEnv:
         call("gca_alex_pack_layers", dev.ptr(self.vegetation), dev.ptr(self.density), dev.ptr(self.dousing),
              dev.ptr(self.vd), dev.ptr(self.dous_bits), E, H, W, dev.stream_ptr(self.device))
 
+    @property
+    def march(self):
+        """True when the packed step runs the marching kernel (W = 256; edge slopes in natural column order)."""
+        return self.slope_layout == "packed" and self.ncols == 256 and self._step_kernel != "tiled"
+
     def _slopes_from(self, altitude):
         E, H, W = self.num_envs, self.nrows, self.ncols
         st = dev.stream_ptr(self.device)
-        if self.slope_layout == "edge":
+        if self.slope_layout == "edge" or self.march:
             call("gca_alex_edge_slope_from_altitude", dev.ptr(altitude), dev.ptr(self.slope_data), E, H, W, st)
         elif self.slope_layout == "packed":
             import torch
@@ -352,7 +366,8 @@ class AdvancedForestFireBulldozerEnv:
     def _context(self):
         """The reference's context dict (advanced_bulldozer.py:109-129, :711-743) over device views.
         Layout differences: "key" is the per-env Philox step counter (the JAX PRNG key's role), "slope" the
-        step's slope layout (edge values (E, 4, H, W), coalesced when packed, or p_slope planes (E, 8, H, W)
+        step's slope layout (edge values (E, 4, H, W), coalesced when packed off W = 256, or p_slope planes
+        (E, 8, H, W)
         instead of (E, H, W, 3, 3)), "fire_age" i16, "true_grid" / "dousing_count" / "vegetation" / "density"
         u8; "altitude" is None without hidden layers."""
         per_env = {"wind_index": self.wind_index, "density": self.density, "vegetation": self.vegetation,
@@ -623,13 +638,14 @@ class AdvancedForestFireBulldozerEnv:
                     dev.ptr(self.age[a]), dev.ptr(self.age[b]), dev.ptr(self.vd), dev.ptr(self.dous_bits),
                     dev.ptr(self.slope_data), dev.ptr(self.wind_index), dev.ptr(self.rng_step), dev.ptr(self.counts),
                     dev.ptr(None if self.act is None else self.act[a]), dev.ptr(None if self.act is None else self.act[b]))
+            fn = "gca_alex_step_march" if self.march else "gca_alex_step_packed"
             if render:
                 if not self.fused_observation:
                     raise ValueError("ca_step(render=True) needs fused_observation")
-                call("gca_alex_step_packed_rgb", *args, dev.ptr(self.obs_colors), dev.ptr(self.is_night),
-                     dev.ptr(self.rgb), dev.stream_ptr(self.device))
+                call(fn + "_rgb", *args, dev.ptr(self.obs_colors), dev.ptr(self.is_night), dev.ptr(self.rgb),
+                     dev.stream_ptr(self.device))
             else:
-                call("gca_alex_step_packed", *args, dev.stream_ptr(self.device))
+                call(fn, *args, dev.stream_ptr(self.device))
             self._pinecones(a, b)
             self.cur = b
             return

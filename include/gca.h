@@ -194,6 +194,19 @@ int gca_alex_step_packed_rgb(const gca_alex_params* p, int E, int H, int W, cons
                              const float* edge_slope_coal, const int32_t* wind_index, const uint32_t* rng_step,
                              int32_t* counts, const uint8_t* act_in, uint8_t* act_out, const float* color_table,
                              const int32_t* is_night, float* rgb, void* stream);
+/* gca_alex_step_packed / _rgb in marching form for W == 256 (H % 16 == 0): one wave walks one 16 x 256 tile row by
+ * row (gca_alex_march.hip), every slope byte read once. Same replaced code, arguments, results (bit for bit), tile
+ * activity map and frame, except edge_slope: the edge layout (E,4,H,W) in natural column order (the output of
+ * gca_alex_edge_slope_from_altitude, not coalesced). */
+int gca_alex_step_march(const gca_alex_params* p, int E, int H, int W, const uint8_t* grid_in, uint8_t* grid_out,
+                        const int16_t* age_in, int16_t* age_out, const uint8_t* vd, const uint16_t* dous_bits,
+                        const float* edge_slope, const int32_t* wind_index, const uint32_t* rng_step, int32_t* counts,
+                        const uint8_t* act_in, uint8_t* act_out, void* stream);
+int gca_alex_step_march_rgb(const gca_alex_params* p, int E, int H, int W, const uint8_t* grid_in, uint8_t* grid_out,
+                            const int16_t* age_in, int16_t* age_out, const uint8_t* vd, const uint16_t* dous_bits,
+                            const float* edge_slope, const int32_t* wind_index, const uint32_t* rng_step,
+                            int32_t* counts, const uint8_t* act_in, uint8_t* act_out, const float* color_table,
+                            const int32_t* is_night, float* rgb, void* stream);
 /* vd (nullable) and dous_bits of gca_alex_step_packed from veg / den / dousing (E,H,W) u8; W % 16 == 0. */
 int gca_alex_pack_layers(const uint8_t* veg, const uint8_t* den, const uint8_t* dousing, uint8_t* vd,
                          uint16_t* dous_bits, int E, int H, int W, void* stream);

@@ -10,7 +10,7 @@ O=$R/gym-cellular-automata_amd/gymca_amd/_lib/variants
 B=$C/build/variant_$NAME
 mkdir -p $O $B
 F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -Wno-unused-function -munsafe-fp-atomics $*"
-for s in gca_util gca_windy gca_env gca_alex gca_ds gca_obs gca_pine gca_init; do
+for s in gca_util gca_windy gca_env gca_alex gca_alex_march gca_ds gca_obs gca_pine gca_init; do
   /opt/rocm/bin/hipcc $F -c $C/$s.hip -o $B/$s.o &
 done
 wait

@@ -20,7 +20,7 @@ import shutil
 import sys
 from collections import defaultdict
 
-KERNELS = {"alex_step_kernel": "alex_step", "windy_fast_kernel": "windy_fast", "windy_exact_kernel": "windy_exact",
+KERNELS = {"alex_step_kernel": "alex_step", "alex_march_kernel": "alex_march", "windy_fast_kernel": "windy_fast", "windy_exact_kernel": "windy_exact",
            "windy_rows_kernel": "windy_rows", "adv_obs_plain_kernel": "adv_obs_plain",
            "count_kernel": "count", "advenv_post_kernel": "advenv_post",
            "adv_observation_kernel": "adv_observation", "random_actions_kernel": "random_actions"}

@@ -1,0 +1,167 @@
+"""GPU parity of the marching Alexandridis step (gca_alex_step_march / _rgb, gca_alex_march.hip): bit-identical to the
+tiled packed step (gca_alex_step_packed / _rgb) on the same state for every burn radius, with and without growth, over
+several steps, through the tile activity map and the fused frame, and to the C oracle on the unpacked state."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from alex_cases import make_case
+from oracle import alex_c
+from test_gpu_edge_slope import _t, altitude, params, slopes
+
+pytestmark = pytest.mark.gpu
+
+
+def _layers(device, case):
+    import torch
+
+    from gymca_amd import _device as dev
+    from gymca_amd._lib import call
+
+    E, H, W = case["grid"].shape
+    veg, den, dous = (_t(case[k], torch.uint8, device) for k in ("veg", "den", "dous"))
+    vd = torch.empty_like(veg)
+    bits = torch.empty((E, H * W // 16), dtype=torch.int16, device=device)
+    call("gca_alex_pack_layers", dev.ptr(veg), dev.ptr(den), dev.ptr(dous), dev.ptr(vd), dev.ptr(bits), E, H, W,
+         dev.stream_ptr())
+    return vd, bits
+
+
+def _run(device, fn, p, case, slope, rng_step, vd, bits, act_in=None, rgb=None, night=None):
+    """One step through `fn` (packed or march, plain or _rgb); returns the host copies of its outputs."""
+    import torch
+
+    from gymca_amd import _device as dev
+    from gymca_amd._lib import call
+
+    E, H, W = case["grid"].shape
+    g, a = _t(case["grid"], torch.uint8, device), _t(case["age"], torch.int16, device)
+    wi = _t(case["widx"], torch.int32, device)
+    rs = _t(np.asarray(rng_step, np.uint32).view(np.int32), torch.int32, device)
+    go, ao = torch.empty_like(g), torch.empty_like(a)
+    counts = torch.zeros((E, 3), dtype=torch.int32, device=device)
+    tiles = (H // 16) * (W // 256)
+    ain = None if act_in is None else _t(act_in, torch.uint8, device)
+    aout = torch.full((E, tiles), 7, dtype=torch.uint8, device=device)
+    args = [p, E, H, W, dev.ptr(g), dev.ptr(go), dev.ptr(a), dev.ptr(ao), dev.ptr(vd), dev.ptr(bits), dev.ptr(slope),
+            dev.ptr(wi), dev.ptr(rs), dev.ptr(counts), dev.ptr(ain), dev.ptr(aout)]
+    out_rgb = None
+    if rgb is not None:
+        col, nt = rgb
+        out_rgb = torch.full((E, H, W, 3), -1.0, dtype=torch.float32, device=device)
+        args += [dev.ptr(col), dev.ptr(nt), dev.ptr(out_rgb)]
+    call(fn, *args, dev.stream_ptr())
+    torch.cuda.synchronize()
+    return (go.cpu().numpy(), ao.cpu().numpy(), counts.cpu().numpy(), aout.cpu().numpy(),
+            None if out_rgb is None else out_rgb.cpu().numpy())
+
+
+def _coalesced(device, es):
+    import torch
+
+    from gymca_amd import _device as dev
+    from gymca_amd._lib import call
+
+    E, _, H, W = es.shape
+    coal = torch.empty_like(es)
+    call("gca_alex_edge_slope_coalesce", dev.ptr(es), dev.ptr(coal), E, H, W, dev.stream_ptr())
+    return coal
+
+
+def _with_radius(p, R):
+    q = type(p)()
+    ctypes.memmove(ctypes.addressof(q), ctypes.addressof(p), ctypes.sizeof(q))
+    q.R = R
+    return q
+
+
+@pytest.mark.parametrize("R", [1, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("E,H,seed,p_tree", [(2, 256, 41, 0.0), (3, 48, 42, 0.01), (2, 16, 43, 0.0)])
+def test_march_matches_packed(device, R, E, H, seed, p_tree):
+    """Grid, ages, counts and the activity map out of the marching step equal the tiled step's, three steps on."""
+    W = 256
+    case = make_case(E, H, W, seed, p_tree=p_tree, dousing_p=0.2, fire_p=0.05)
+    p = _with_radius(params(H, p_tree, seed=seed * 5), R)
+    es, _ = slopes(device, altitude(E, H, W, seed))
+    coal = _coalesced(device, es)
+    vd, bits = _layers(device, case)
+    for s in range(3):
+        rs = np.full(E, 7 * s + 2, np.uint32)
+        g0, a0, c0, t0, _ = _run(device, "gca_alex_step_packed", p, case, coal, rs, vd, bits)
+        g1, a1, c1, t1, _ = _run(device, "gca_alex_step_march", p, case, es, rs, vd, bits)
+        assert np.array_equal(g1, g0), f"R={R} step {s}: {np.argwhere(g1 != g0)[:5]}"
+        assert np.array_equal(a1, a0), f"R={R} step {s}: ages {np.argwhere(a1 != a0)[:5]}"
+        assert np.array_equal(c1, c0)
+        assert np.array_equal(t1, t0)
+        case["grid"], case["age"] = g1, a1
+
+
+def test_march_tile_skip_and_frame(device):
+    """act_in with fire-free tiles (copied) and the fused RGB frame: equal to the tiled kernel's, both night and
+    day, and the skipped tiles' frame equals the frame of the full step."""
+    import torch
+
+    from gymca_amd import _device as dev
+    from gymca_amd._lib import call
+    from gymca_amd.forest_fire.bulldozer.observation import make_obs_params
+
+    E, H, W = 3, 128, 256
+    case = make_case(E, H, W, 51, p_tree=0.0, dousing_p=0.2, fire_p=0.0)
+    # fire only in tile rows 2 and 6 of env 0, tile row 4 of env 2; env 1 has none
+    case["grid"][0, 40, 10:20] = 2
+    case["grid"][0, 100, 200] = 2
+    case["grid"][2, 70, 0:256:9] = 2
+    case["age"][case["grid"] == 2] = 3
+    p = params(H, 0.0, seed=9)
+    es, _ = slopes(device, altitude(E, H, W, 51))
+    coal = _coalesced(device, es)
+    vd, bits = _layers(device, case)
+    tiles = H // 16
+    act = np.zeros((E, tiles), np.uint8)
+    for e in range(E):
+        for t in range(tiles):
+            act[e, t] = int((case["grid"][e, 16 * t:16 * t + 16] == 2).any())
+    op = make_obs_params(0, 1, 2, False, False, 8)
+    col = torch.zeros((12, 4), dtype=torch.float32, device=device)
+    call("gca_obs_color_table", op, dev.ptr(col), dev.stream_ptr())
+    night = torch.as_tensor(np.array([0, 1, 1], np.int32), device=device)
+    rs = np.full(E, 3, np.uint32)
+    ref = _run(device, "gca_alex_step_packed_rgb", p, case, coal, rs, vd, bits, act_in=act, rgb=(col, night))
+    got = _run(device, "gca_alex_step_march_rgb", p, case, es, rs, vd, bits, act_in=act, rgb=(col, night))
+    full = _run(device, "gca_alex_step_march_rgb", p, case, es, rs, vd, bits, act_in=None, rgb=(col, night))
+    for k in range(4):
+        assert np.array_equal(got[k], ref[k]), k
+        assert np.array_equal(full[k][:3], ref[k][:3]) if k < 3 else True
+    assert np.array_equal(got[4], ref[4])
+    assert np.array_equal(full[4], ref[4])
+    assert (got[3][1] == 0).all() and got[3][0].any()
+
+
+def test_march_matches_oracle(device):
+    """The marching step against the C oracle (Philox mode) on the unpacked state, directly."""
+    E, H, W = 2, 64, 256
+    case = make_case(E, H, W, 61, p_tree=0.01, dousing_p=0.2, fire_p=0.05)
+    p = params(H, 0.01, seed=77)
+    es, ps = slopes(device, altitude(E, H, W, 61))
+    vd, bits = _layers(device, case)
+    rs = np.full(E, 11, np.uint32)
+    g1, a1, c1, _, _ = _run(device, "gca_alex_step_march", p, case, es, rs, vd, bits)
+    go, ao, co, _ = alex_c.alex_step(p, case["grid"], case["age"], case["veg"], case["den"],
+                                     case["dous"], ps.cpu().numpy(), case["widx"], rng_step=rs)
+    assert np.array_equal(g1, go), np.argwhere(g1 != go)[:5]
+    assert np.array_equal(a1, ao)
+    assert np.array_equal(c1, co)
+
+
+def test_march_rejects_bad_shapes(device):
+    import torch
+
+    from gymca_amd import _device as dev
+    from gymca_amd._lib import GCAError, call
+
+    p = params(16)
+    g = torch.zeros((1, 16, 512), dtype=torch.uint8, device=device)
+    with pytest.raises(GCAError):
+        call("gca_alex_step_march", p, 1, 16, 512, dev.ptr(g), dev.ptr(g.clone()), dev.ptr(g), dev.ptr(g), dev.ptr(g),
+             dev.ptr(g), dev.ptr(g), dev.ptr(g), None, None, None, None, dev.stream_ptr())

@@ -158,9 +158,10 @@ def test_headline_sizes_injected_vs_reference_rule(device, N, seed):
     1. gca_alex_step (8 p_slope planes) and gca_alex_step_es (edge slopes) vs the numpy restatement of
        _update_grid (ca_alexandridis_jax.py:62,108-153,345-349,379-398) and the float64 probability;
     2. the two layouts bit-identical (states, ages, counts, probabilities);
-    3. the headline kernel, gca_alex_step_packed (Philox mode, packed layout), bit-identical to
-       gca_alex_step_es in Philox mode on the same state, whose probabilities are bit-identical to the
-       injected-mode probabilities checked in 1 — so the timed kernel evaluates the reference's p_d."""
+    3. the headline kernels, gca_alex_step_packed (tiled) and at W = 256 gca_alex_step_march (the env's step
+       there; Philox mode, packed layout), bit-identical to gca_alex_step_es in Philox mode on the same state,
+       whose probabilities are bit-identical to the injected-mode probabilities checked in 1 — so the timed
+       kernel evaluates the reference's p_d."""
     import torch
 
     from gymca_amd import _device as dev
@@ -198,6 +199,12 @@ def test_headline_sizes_injected_vs_reference_rule(device, N, seed):
     g_es, a_es, c_es, po_es = step(device, "gca_alex_step_es", p, case_ph, es, rng_step=rs, probs=True)
     g_pk, a_pk, c_pk, _, _ = packed_step(device, p, case_ph, es, rs)
     assert np.array_equal(g_pk, g_es) and np.array_equal(a_pk, a_es) and np.array_equal(c_pk, c_es)
+    if N == 256:
+        from test_gpu_alex_march import _layers, _run
+
+        vd, bits = _layers(device, case_ph)
+        g_mr, a_mr, c_mr, _, _ = _run(device, "gca_alex_step_march", p, case_ph, es, rs, vd, bits)
+        assert np.array_equal(g_mr, g_es) and np.array_equal(a_mr, a_es) and np.array_equal(c_mr, c_es)
     _, _, _, po_inj = step(device, "gca_alex_step_es", p, case_ph, es, inj=inj, probs=True)
     assert np.array_equal(po_es.view(np.uint32), po_inj.view(np.uint32))
 
@@ -411,7 +418,7 @@ def test_philox_and_injected_modes_share_probabilities(device):
 
 
 def test_packed_fast_kernel_burn_law_chi_square(device):
-    """The timed kernel (gca_alex_step_packed: MODE 0, FAST, edge slopes, packed layout) against the
+    """The timed kernel (the env's packed-layout step at 256^2: gca_alex_step_march) against the
     reference's burn law. The reference ignites a TREE iff some burning neighbour d has u_d < p_d with
     independent uniforms (ca_alexandridis_jax.py:379-383), i.e. with probability 1 - prod_d (1 - clamp01(p_d));
     the kernel draws one uniform against that product. 32 envs x 256^2 mid-episode states (hidden layers,
@@ -449,7 +456,8 @@ def test_packed_fast_kernel_burn_law_chi_square(device):
     for t in range(T):
         age_buf.copy_(age0)  # the packed step updates ages in place
         rs = torch.full((E,), 1000 + t, dtype=torch.int32, device=device)
-        call("gca_alex_step_packed", env.alex_params, E, N, N, dev.ptr(g_in), dev.ptr(g_out), dev.ptr(age_buf),
+        assert env.march
+        call("gca_alex_step_march", env.alex_params, E, N, N, dev.ptr(g_in), dev.ptr(g_out), dev.ptr(age_buf),
              dev.ptr(age_buf), dev.ptr(env.vd), dev.ptr(env.dous_bits), dev.ptr(env.slope_data), dev.ptr(env.wind_index),
              dev.ptr(rs), dev.ptr(counts), None, None, st)
         burned += ((g_out == 2) & (g_in == 1)).to(torch.int32)
