@@ -78,21 +78,8 @@ __device__ __forceinline__ void window4(uint32_t X, int k, uint32_t (&B)[4]) {
 
 __device__ __forceinline__ float4 ldf4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 // *(T*)((char*)base + off): a wave-uniform base and a 32-bit lane byte offset (global_load ... v_off, s[base])
-#ifndef GCA_MARCH_SBASE
-#define GCA_MARCH_SBASE 0
-#endif
-#ifndef GCA_MARCH_OBS_MODE
-#define GCA_MARCH_OBS_MODE 0  // fused frame: 0 = through the wave's LDS row (1 KiB per store), 1 / 2 = per-lane 48 B (nt / plain)
-#endif
 template <class T, class B> __device__ __forceinline__ T ld_at(const B* base, uint32_t off) {
-    if (!GCA_MARCH_SBASE) return *reinterpret_cast<const T*>(reinterpret_cast<const unsigned char*>(base) + off);
-    // (A/B hook GCA_MARCH_SBASE) the base through readfirstlane (a no-op on an SGPR value): hipcc otherwise folds loop-invariant parts of the
-    // uniform base into 64-bit VGPR offsets (8 extra VGPR pairs and a v_lshl_add_u64 per load)
-    const uint64_t b = (uint64_t)(uintptr_t)base;
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b), hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
-    typedef const __attribute__((address_space(1))) unsigned char* gptr;  // global, not flat
-    const gptr sb = (gptr)(((uint64_t)hi << 32) | lo);
-    return *reinterpret_cast<const T*>((const unsigned char*)(sb + off));  // (address space inferred: global)
+    return *reinterpret_cast<const T*>(reinterpret_cast<const unsigned char*>(base) + off);
 }
 typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
 typedef int16_t i16x2 __attribute__((ext_vector_type(2)));
@@ -151,48 +138,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     auto dflags = [&](uint32_t w16) -> uint32_t { return gca_spread4(w16 >> (4 * (lane & 3))); };
     // RGB row r of the lane's 4 cells (kinds from the new TREE / FIRE nibbles, pre-step dousing flags) through the
     // wave's LDS row: 48 B per lane in, 3 x 1 KiB contiguous non-temporal stores out
+    // The RGB row r of the lane's 4 cells (kinds from the new TREE / FIRE nibbles, pre-step dousing flags) through the
+    // wave's LDS row: the 4 colours read back to back (one index byte per cell: 2 * kind + dousing), 3 x 16 B written,
+    // then 3 x 1 KiB contiguous non-temporal stores (r03k: two rows per flush, or plain stores, measured slower)
     auto write_rgb_row = [&](int r, uint32_t tB, uint32_t fB, uint32_t dfl) {
-        if constexpr (OBS && GCA_MARCH_OBS_MODE != 0) {  // (A/B hook) each lane stores its own 48 B: 3 x 16 B
-            typedef float f4t __attribute__((ext_vector_type(4)));
-            float c[12];
+        if constexpr (OBS) {
+            const uint32_t kidx = 2u * gca_spread4(tB) + 4u * gca_spread4(fB) + (dfl & 0x01010101u);
+            float4 c[4];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int kind = ((tB >> j) & 1u) ? 1 : (((fB >> j) & 1u) ? 2 : 0);
-                const float4 cl = colw[wl][2 * kind + (int)((dfl >> (8 * j)) & 1u)];
-                c[3 * j] = cl.x;
-                c[3 * j + 1] = cl.y;
-                c[3 * j + 2] = cl.z;
-            }
-            f4t* dst = reinterpret_cast<f4t*>(obs.rgb + ((size_t)e * H + r) * (MW * 3) + 12 * lane);
-#pragma unroll
-            for (int t = 0; t < 3; ++t) {
-                const f4t v = {c[4 * t], c[4 * t + 1], c[4 * t + 2], c[4 * t + 3]};
-                if (GCA_MARCH_OBS_MODE == 1)
-                    __builtin_nontemporal_store(v, dst + t);
-                else
-                    dst[t] = v;
-            }
-        } else if constexpr (OBS) {
-            // one cell at a time (a colour is 4 VGPRs): cell j's RGB at byte 48 * lane + 12 * j of the row image
-            float* im = reinterpret_cast<float*>(img[wl]) + 12 * lane;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int kind = ((tB >> j) & 1u) ? 1 : (((fB >> j) & 1u) ? 2 : 0);
-                const float4 cl = colw[wl][2 * kind + (int)((dfl >> (8 * j)) & 1u)];
-                im[3 * j] = cl.x;
-                im[3 * j + 1] = cl.y;
-                im[3 * j + 2] = cl.z;
-            }
+            for (int j = 0; j < 4; ++j) c[j] = colw[wl][(kidx >> (8 * j)) & 0xFFu];
+            float4* im = img[wl] + 3 * lane;
+            im[0] = make_float4(c[0].x, c[0].y, c[0].z, c[1].x);
+            im[1] = make_float4(c[1].y, c[1].z, c[2].x, c[2].y);
+            im[2] = make_float4(c[2].z, c[3].x, c[3].y, c[3].z);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             typedef float f4t __attribute__((ext_vector_type(4)));
             float* row = obs.rgb + ((size_t)e * H + r) * (MW * 3);
+            float4 v[3];
 #pragma unroll
-            for (int t = 0; t < 3; ++t) {
-                const float4 v = img[wl][64 * t + lane];
-                __builtin_nontemporal_store((f4t){v.x, v.y, v.z, v.w}, reinterpret_cast<f4t*>(row + 4 * (64 * t + lane)));
-            }
+            for (int t = 0; t < 3; ++t) v[t] = img[wl][64 * t + lane];
+#pragma unroll
+            for (int t = 0; t < 3; ++t)
+                __builtin_nontemporal_store((f4t){v[t].x, v[t].y, v[t].z, v[t].w},
+                                            reinterpret_cast<f4t*>(row + 4 * (64 * t + lane)));
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // this row's reads before the next row's writes
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -317,8 +287,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
             nVD = ld_at<uint32_t>(vE + r1 * MW, lc);
             nAge = ld_at<uint2>(aE + r1 * MW, lane_a);
         }
+        // Row r+2's slope planes (loaded during this row) serve rows r+1 and r+2, which can only need them with a FIRE
+        // in rows r..r+3: without one anywhere in the tile's columns the load re-reads the strip's first row instead
+        // (an L2 hit, no HBM traffic; a branch around the load would keep SC live and cost registers) and the values
+        // are never used (those rows' row_need is false). The ring holds rows up to r+R; R < 3 always loads.
+        bool need_next = true;
         auto load_next_slopes = [&]() {  // row r+2's raw planes into SC
-            const size_t rs = (size_t)min(r + 2, H - 1);
+            const size_t rs = need_next ? (size_t)min(r + 2, H - 1) : (size_t)s0;
 #pragma unroll
             for (int k = 0; k < 4; ++k) SC[k] = ld_at<float4>(sE + (size_t)k * HW + rs * MW, lane_s);
         };
@@ -343,6 +318,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
             fm1 = rw[R];
             f0 = rw[R + 1];
             fp1 = rw[R + 2];
+            if constexpr (R >= 3) need_next = __ballot((rw[R + 1] | rw[R + 2] | rw[R + 3] | rw[R + 4]) != 0u) != 0ull;
         }
         dring[5] = dflags(dnew);
         Dv1 += dring[4] - dring[1];
@@ -350,21 +326,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
 
         // ---- masks of the row: own kinds, FIRE neighbourhood (3 rows x 6 columns per lane)
         const uint32_t treeB = gca_eq_nib(own, Tp), emptyB = gca_eq_nib(own, Ep);
-        const uint32_t nib3 = ((fm1 * 0x01020408u) >> 24) | (((f0 * 0x01020408u) >> 24) << 8) |
-                              (((fp1 * 0x01020408u) >> 24) << 16);
-        const uint32_t fireB = (nib3 >> 8) & 0xFu;
-        const uint32_t ext = ((from_prev(nib3) >> 3) & 0x010101u) | ((nib3 & 0x0F0F0Fu) << 1) |
-                             ((from_next(nib3) & 0x010101u) << 5);
-        auto dir_shift = [](int d) -> int {  // bit of ext holding direction d of the lane's cell 0
-            const int a = d < 3 ? 0 : (d < 5 ? 1 : 2);
-            const int b = d < 3 ? d : (d == 3 ? 0 : (d == 4 ? 2 : d - 5));
-            return 8 * a + b;
+        // burning-neighbour masks: 0xFF in byte j iff cell j's neighbour d is FIRE, from the row dwords shifted one
+        // column across lanes ([prev.b3, X.b0..b2] / [X.b1..b3, next.b0]); built per direction inside the pass (8
+        // live masks cost registers), and masked into the products with one SDWA v_and per cell
+        auto shl_c = [](uint32_t x) { return __builtin_amdgcn_alignbyte(x, from_prev(x), 3); };  // column c-1
+        auto shr_c = [](uint32_t x) { return __builtin_amdgcn_alignbyte(from_next(x), x, 1); };  // column c+1
+        auto dir_mask = [&](int d) -> uint32_t {
+            const uint32_t row = d < 3 ? fm1 : (d < 5 ? f0 : fp1);
+            const int dc = d < 3 ? d - 1 : (d == 3 ? -1 : (d == 4 ? 1 : d - 6));
+            uint32_t m = dc < 0 ? shl_c(row) : (dc > 0 ? shr_c(row) : row);
+            m *= 0xFFu;
+            asm volatile("" : "+v"(m));  // opaque: hipcc would fold the byte extractions into per-byte multiplies
+            return m;
         };
-        uint32_t anyfire = 0u;
-#pragma unroll
-        for (int d = 0; d < 8; ++d) anyfire |= ext >> dir_shift(d);
-        anyfire &= 0xFu;
-
+        const uint32_t fireB = (f0 * 0x01020408u) >> 24;
+        // a FIRE anywhere in the 3 x 3 block (the centre too: it only matters for TREE cells, which are not FIRE)
+        const uint32_t vor = fm1 | f0 | fp1;
+        const uint32_t anyfire = (((vor | shl_c(vor) | shr_c(vor)) & 0x01010101u) * 0x01020408u) >> 24;
         gca_f2 qn[2] = {{1.0f, 1.0f}, {1.0f, 1.0f}};
         const bool row_need = __ballot((treeB & anyfire) != 0u) != 0ull;
         const bool kill_row = r == 0 || r == H - 1;       // every factor of row r is 1
@@ -433,17 +411,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
                     // pin base and the product: otherwise the direction-independent work of all 8 directions is
                     // hoisted (as in gca_alex.hip)
                     asm volatile("" : "+v"(ph[0]), "+v"(ph[1]), "+v"(qn[0]), "+v"(qn[1]));
-                    const int sh = dir_shift(d);
                     const gca_f2 wd2 = {wind[d], wind[d]};
+                    const uint32_t Md = dir_mask(d);
 #pragma unroll
                     for (int h = 0; h < 2; ++h) {
                         const gca_f2 t = ph[h] * wd2;
                         const gca_f2 c = KILL ? (gca_f2){gca_clamp01(t.x), gca_clamp01(t.y)}
                                               : gca_pk_mul_clamp01(t, (gca_f2){a[2 * h], a[2 * h + 1]});
-                        const gca_f2 x = (gca_f2){1.0f, 1.0f} - c;
-                        const uint32_t x0 = gca_bfi32(gca_sbit(ext, sh + 2 * h), __float_as_uint(x.x), 0x3F800000u);
-                        const uint32_t x1 = gca_bfi32(gca_sbit(ext, sh + 2 * h + 1), __float_as_uint(x.y), 0x3F800000u);
-                        qn[h] = qn[h] * (gca_f2){__uint_as_float(x0), __uint_as_float(x1)};
+                        // no burning neighbour d: c -> +0, x = 1 - 0 = 1 exactly (the oracle skips the factor)
+                        const uint32_t c0 = __float_as_uint(c.x) & (uint32_t)(int32_t)(int8_t)(Md >> (16 * h));
+                        const uint32_t c1 = __float_as_uint(c.y) & (uint32_t)(int32_t)(int8_t)(Md >> (16 * h + 8));
+                        const gca_f2 x = (gca_f2){1.0f, 1.0f} - (gca_f2){__uint_as_float(c0), __uint_as_float(c1)};
+                        qn[h] = qn[h] * x;
                     }
                     __builtin_amdgcn_sched_barrier(0);
                 };

@@ -64,11 +64,10 @@ __device__ __forceinline__ double u01_f64(uint32_t hi, uint32_t lo) {
     const uint64_t v = (((uint64_t)hi << 32) | lo) >> 11;
     return (double)v * 0x1.0p-53;
 }
-// Integer in [lo, hi) by multiply-shift (hi <= lo -> lo).
+// Integer in [lo, hi) by multiply-shift (hi <= lo -> lo): branch-free, span 0 gives lo (one v_mul_hi_u32 + add).
 __device__ __forceinline__ int32_t randint_ms(uint32_t x, int32_t lo, int32_t hi) {
-    if (hi <= lo) return lo;
-    const uint32_t span = (uint32_t)(hi - lo);
-    return lo + (int32_t)(((uint64_t)x * span) >> 32);
+    const uint32_t span = hi > lo ? (uint32_t)(hi - lo) : 0u;
+    return lo + (int32_t)__umulhi(x, span);
 }
 
 // WindyForestFire active-direction mask (ca_windy.py:53-77): bit d set iff roll[d] < wind[d]
