@@ -787,8 +787,8 @@ __global__ __launch_bounds__(NT, GCA_ALEX_WGS) void alex_step_kernel(
 
     // ---- direction-outer pass: each p_slope row segment (16 floats = 64 B per lane, 1 KiB per
     //      16 lanes) is read in one burst, so every HBM line is consumed by one wave instruction group.
-    //      qn = prod over burning directions of (1 - clamp01(p_d)); a non-burning direction multiplies
-    //      by exactly 1.0f (bit-select), so the product equals the oracle's skip-form.
+    //      qn = prod over burning directions of (1 - clamp01(p_d)), each factor applied as qn = fma(-qn, c, qn);
+    //      a non-burning direction's c is masked to +0 (qn unchanged exactly), the oracle's skip-form.
     f2 qn2[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) qn2[j] = (f2){1.0f, 1.0f};
@@ -923,10 +923,11 @@ __global__ __launch_bounds__(NT, GCA_ALEX_WGS) void alex_step_kernel(
                     c = pk_mul_clamp01(t, ps);
                 }
                 if (!INJECT) {
-                    const f2 x = (f2){1.0f, 1.0f} - c;
-                    const uint32_t x0 = bfi32(sbit(fbd, 2 * j), __float_as_uint(x.x), 0x3F800000u);
-                    const uint32_t x1 = bfi32(sbit(fbd, 2 * j + 1), __float_as_uint(x.y), 0x3F800000u);
-                    qn2[j] = qn2[j] * (f2){__uint_as_float(x0), __uint_as_float(x1)};
+                    // q <- fma(-q, c, q) = q * (1 - c) with one rounding; a non-burning direction has c masked to +0,
+                    // so q is unchanged exactly (the oracle skips the factor)
+                    const uint32_t c0 = __float_as_uint(c.x) & sbit(fbd, 2 * j);
+                    const uint32_t c1 = __float_as_uint(c.y) & sbit(fbd, 2 * j + 1);
+                    qn2[j] = __builtin_elementwise_fma(-qn2[j], (f2){__uint_as_float(c0), __uint_as_float(c1)}, qn2[j]);
                 }
             }
 #pragma unroll

@@ -53,7 +53,11 @@ __host__ __device__ constexpr uint32_t win_mask(int o, int j, int k) {
     }
     return m;
 }
-// B[j] = sum of the byte counts X over columns 4l+j-k .. 4l+j+k (k <= 8: lanes l-2 .. l+2)
+// is dword o (lane l+o) entirely inside the window of radius k around column j?
+__host__ __device__ constexpr bool win_full(int o, int j, int k) { return j - k <= 4 * o && 4 * o + 3 <= j + k; }
+// B[j] = sum of the byte counts X over columns 4l+j-k .. 4l+j+k (k <= 8: lanes l-2 .. l+2), v_dot4_u32_u8 chains. The
+// dwords a window covers fully (always a run around the lane's own: {0}, {-1,0}, {0,1} or {-1,0,1} for k >= 2) are summed
+// once and shared by the four windows; the partial dwords are added with their byte masks (k = 6: 10 dot4 instead of 16)
 __device__ __forceinline__ void window4(uint32_t X, int k, uint32_t (&B)[4]) {
     uint32_t n[5] = {0u, 0u, X, 0u, 0u};
     if (k >= 1) {
@@ -64,11 +68,30 @@ __device__ __forceinline__ void window4(uint32_t X, int k, uint32_t (&B)[4]) {
         n[0] = from_prev(n[1]);
         n[4] = from_next(n[3]);
     }
+    constexpr uint32_t ONES = 0x01010101u;
+    // which full runs the four windows use (compile-time after unrolling)
+    bool use0 = false, useL = false, useR = false, useLR = false;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        uint32_t acc = 0u;
+        const bool f0 = win_full(0, j, k), fl = win_full(-1, j, k), fr = win_full(1, j, k);
+        if (f0 && fl && fr) useLR = true;
+        else if (f0 && fl) useL = true;
+        else if (f0 && fr) useR = true;
+        else if (f0) use0 = true;
+    }
+    uint32_t S0 = 0u, SL = 0u, SR = 0u, SLR = 0u;
+    if (use0 || useL || useR || useLR) S0 = __builtin_amdgcn_udot4(n[2], ONES, 0u, false);
+    if (useL || useLR) SL = __builtin_amdgcn_udot4(n[1], ONES, S0, false);
+    if (useR) SR = __builtin_amdgcn_udot4(n[3], ONES, S0, false);
+    if (useLR) SLR = __builtin_amdgcn_udot4(n[3], ONES, SL, false);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const bool f0 = win_full(0, j, k), fl = win_full(-1, j, k), fr = win_full(1, j, k);
+        const bool run = f0;  // the full dwords of a window with the lane's own are a run containing it
+        uint32_t acc = !run ? 0u : (fl && fr) ? SLR : fl ? SL : fr ? SR : S0;
 #pragma unroll
         for (int o = -2; o <= 2; ++o) {
+            if (run && (o == 0 || (o == -1 && fl) || (o == 1 && fr))) continue;  // inside the shared sum
             const uint32_t m = win_mask(o, j, k);
             if (m) acc = __builtin_amdgcn_udot4(n[o + 2], m, acc, false);
         }
@@ -403,7 +426,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
                 const gca_f2 ad = {lut[wl][8 + (b0 >> 4)], lut[wl][8 + (b1 >> 4)]};
                 ph[h] = (ph[h] * av) * ad;
             }
-            // ---- directions, in order: qn = prod over burning d of (1 - clamp01(base * wind[d] * p_slope[d]));
+            // ---- directions, in order: qn = prod over burning d of (1 - clamp01(base * wind[d] * p_slope[d])), each
+            //      factor as qn = fma(-qn, c, qn);
             //      rows 0 and H-1 (KILL: every factor 1, no edge arithmetic) take their own copy of the pass
             auto dir_pass = [&](auto kill_tag) {
                 constexpr bool KILL = decltype(kill_tag)::value;
@@ -418,11 +442,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
                         const gca_f2 t = ph[h] * wd2;
                         const gca_f2 c = KILL ? (gca_f2){gca_clamp01(t.x), gca_clamp01(t.y)}
                                               : gca_pk_mul_clamp01(t, (gca_f2){a[2 * h], a[2 * h + 1]});
-                        // no burning neighbour d: c -> +0, x = 1 - 0 = 1 exactly (the oracle skips the factor)
+                        // qn <- fma(-qn, c, qn) = qn * (1 - c), one rounding (the oracle's order); no burning
+                        // neighbour d: c -> +0 and qn is unchanged exactly (the oracle skips the factor)
                         const uint32_t c0 = __float_as_uint(c.x) & (uint32_t)(int32_t)(int8_t)(Md >> (16 * h));
                         const uint32_t c1 = __float_as_uint(c.y) & (uint32_t)(int32_t)(int8_t)(Md >> (16 * h + 8));
-                        const gca_f2 x = (gca_f2){1.0f, 1.0f} - (gca_f2){__uint_as_float(c0), __uint_as_float(c1)};
-                        qn[h] = qn[h] * x;
+                        qn[h] = __builtin_elementwise_fma(-qn[h], (gca_f2){__uint_as_float(c0), __uint_as_float(c1)}, qn[h]);
                     }
                     __builtin_amdgcn_sched_barrier(0);
                 };

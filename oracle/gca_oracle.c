@@ -14,7 +14,8 @@
  *   p_h   = heat - dous                      (:198)
  *   p_d   = ((((p_h * av) * ad) * wind[d]) * p_slope[d])                       (:206)
  *   injected: TREE -> FIRE iff exists fire neighbour d with u[d] < p_d (:379-383)
- *   philox  : TREE -> FIRE iff u(main) < 1 - prod_{fire d} (1 - clamp01(p_d)), where the cell with
+ *   philox  : TREE -> FIRE iff u(main) < 1 - q, q = prod_{fire d} (1 - clamp01(p_d)) accumulated in d order as
+ *             q = fmaf(-q, clamp01(p_d), q) (one rounding per factor), where the cell with
  *             index lin uses words (2h, 2h+1), h = lin & 1, of Philox(lin >> 1, env, step, ALXC)
  *   EMPTY -> TREE iff u < p_tree; FIRE -> EMPTY iff age <= 1 (age == 1 with burnout_eq1, the
  *   classic ca_alexandridis.py:181-183); ages (:394-423). heat starts at heat0 (0, or the classic
@@ -201,7 +202,7 @@ static void alex_env(const oracle_alex_params* p, int e, int H, int W, const uin
                 if (is_tree) {
                     float qn = 1.0f;
                     for (int q = 0; q < 8; ++q)
-                        if ((fm >> q) & 1u) qn = qn * (1.0f - clamp01(pd[q]));
+                        if ((fm >> q) & 1u) qn = fmaf(-qn, clamp01(pd[q]), qn);
                     burn = u01(main_w) < 1.0f - qn;
                     new_age = randint_ms(aux_w, p->age_lo, p->age_hi);
                 } else {
