@@ -854,24 +854,34 @@ def tiled_kernel_ms(env, device, K=10, reps=3):
     return sorted(times)[len(times) // 2]
 
 
-def measured_traffic(args):
-    """HBM bytes per alex_step launch from the committed rocprofv3 PMC summary
-    (profiles/pmc_traffic.json, written by scripts/pmc_summary.py: 2*FETCH_SIZE + WRITE_SIZE,
-    gfx950 correction) — only when this run is the profiled workload."""
+def _pmc_entry(args):
+    """The committed PMC summary entry (profiles/pmc_traffic.json) of this run's headline kernel, if it is the profiled
+    workload."""
     if args.envs != 4096 or args.size != 256:
         return None
-    tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
-        data = json.load(open(tf))
+        data = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
     except (ValueError, OSError):
         return None
     want = {"packed": "alex_march<6, false>" if args.step_kernel != "tiled" else "alex_step<6, 0, true, true, true>",
             "edge": "alex_step<6, 0, true, true, false>",
             "planes": "alex_step<6, 0, true, false, false>"}[args.slope_layout]
-    for k, v in data.items():  # the Philox-mode FAST kernel at R = 6 (N = 256) of this slope layout
-        if k == want:
-            return v.get("bytes_per_launch")
-    return None
+    return data.get(want)
+
+
+def measured_valu_busy(args):
+    """VALU-busy share of the SIMDs over the headline kernel's launch (profiles/pmc_traffic.json: SQ_ACTIVE_INST_VALU in
+    quad-cycles x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs), scripts/pmc_summary.py)."""
+    e = _pmc_entry(args)
+    return None if e is None else e.get("valu_busy")
+
+
+def measured_traffic(args):
+    """HBM bytes per headline launch from the committed rocprofv3 PMC summary (profiles/pmc_traffic.json, written by
+    scripts/pmc_summary.py: 2*FETCH_SIZE + WRITE_SIZE, the gfx950 correction, calibrated for every load width the
+    kernels issue by scripts/fetch_calib.hip) — only when this run is the profiled workload."""
+    e = _pmc_entry(args)
+    return None if e is None else e.get("bytes_per_launch")
 
 
 def copy_bandwidth(device, nbytes=2 << 30, reps=10):
@@ -960,15 +970,20 @@ def main():
             "episode_start": alex.get("episode_start"),
             "with_rgb_observation": alex.get("with_rgb_observation"),
             "with_rgb_observation_extensions": alex.get("with_rgb_observation_extensions"),
-            # achieved = SURVEY.md §8d's algorithmic figure (41 B per cell-update, "independent of the build's
-            # actual layout") x cells / the kernel's mean launch time; the bytes this build actually moves
-            # (packed layout: 23.125 B/cell) and the PMC traffic are reported beside it
-            "roofline": {"bound": "hbm", "achieved": alex["survey_equiv_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": alex["survey_equiv_gbs"] / HBM_PEAK_GBS, "traffic": traffic,
+            # achieved = the algorithmic bytes of the step as built (23.125 B per cell-update in the packed layout: every
+            # input byte read once, every output byte written once) x cells / the kernel's mean launch time. SURVEY.md
+            # §8d's 41 B (the 8-plane layout's bytes) is reported beside it as survey_equiv_*: since the marching
+            # kernel it exceeds the 8 TB/s peak (> 1.0), i.e. it no longer measures anything. traffic = PMC bytes.
+            "roofline": {"bound": "hbm", "achieved": alex["achieved_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": alex["achieved_gbs"] / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": alex["kernel"],
                          "kernel_ms": alex["kernel_ms"],
                          "tiled_kernel_ms": alex.get("tiled_kernel_ms"),
-                         "algorithmic_bytes_per_cell": ALEX_BYTES_PER_CELL,
+                         "algorithmic_bytes_per_cell": ALEX_BYTES[args.slope_layout],
+                         "survey_bytes_per_cell": ALEX_BYTES_PER_CELL,
+                         "survey_equiv_gbs": alex["survey_equiv_gbs"],
+                         "survey_equiv_frac": alex["survey_equiv_gbs"] / HBM_PEAK_GBS,
+                         "valu_busy": measured_valu_busy(args),
                          "slope_layout": args.slope_layout,
                          "moved_bytes_per_cell": ALEX_BYTES[args.slope_layout],
                          "moved_gbs": alex["achieved_gbs"],

@@ -152,8 +152,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
-    auto graw = [&](int r) -> uint32_t {  // grid bytes of the lane's 4 cells in row r (0 = EMPTY outside)
-        return (r >= 0 && r < H) ? *reinterpret_cast<const uint32_t*>(gE + (uint32_t)r * MW + lc) : 0u;
+    auto graw = [&](int r) -> uint32_t {  // grid bytes of the lane's 4 cells in row r (EMPTY outside the grid)
+        return (r >= 0 && r < H) ? *reinterpret_cast<const uint32_t*>(gE + (uint32_t)r * MW + lc) : Ep;
     };
     auto draw_bits = [&](int r) -> uint32_t {  // the u16 of dousing bits holding the lane's 4 cells
         return (r >= 0 && r < H) ? (uint32_t)dE[(uint32_t)r * (MW / 16) + (uint32_t)(lane >> 2)] : 0u;
@@ -304,19 +304,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
             const size_t r1 = (size_t)min(r + 1, H - 1);
             const uint32_t g = ld_at<uint32_t>(gE + (size_t)min(rg, H - 1) * MW, lc);
             const uint32_t d = ld_at<uint16_t>(dE + (size_t)min(rd, H - 1) * (MW / 16), lane_d);
-            nG = rg < H ? g : 0u;
+            nG = rg < H ? g : Ep;
             nD = rd < H ? d : 0u;
             nOwn = ld_at<uint32_t>(gE + r1 * MW, lc);
             nVD = ld_at<uint32_t>(vE + r1 * MW, lc);
             nAge = ld_at<uint2>(aE + r1 * MW, lane_a);
         }
         // Row r+2's slope planes (loaded during this row) serve rows r+1 and r+2, which can only need them with a FIRE
-        // in rows r..r+3: without one anywhere in the tile's columns the load re-reads the strip's first row instead
-        // (an L2 hit, no HBM traffic; a branch around the load would keep SC live and cost registers) and the values
-        // are never used (those rows' row_need is false). The ring holds rows up to r+R; R < 3 always loads.
-        bool need_next = true;
+        // in rows r..r+3, and only inside the tile (the last row's row r+2 is the next tile's): otherwise the load
+        // re-reads row r+1's planes, which this wave loaded one row ago (an L2 hit, no HBM traffic; a branch around
+        // the load would keep SC live and cost registers), and the values are never used (those rows' row_need is
+        // false). The ring holds rows up to r+R; R < 3 always loads.
+        bool need_next = i + 1 < SH;
         auto load_next_slopes = [&]() {  // row r+2's raw planes into SC
-            const size_t rs = need_next ? (size_t)min(r + 2, H - 1) : (size_t)s0;
+            const size_t rs = (size_t)min(need_next ? r + 2 : r + 1, H - 1);
 #pragma unroll
             for (int k = 0; k < 4; ++k) SC[k] = ld_at<float4>(sE + (size_t)k * HW + rs * MW, lane_s);
         };
@@ -341,7 +342,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
             fm1 = rw[R];
             f0 = rw[R + 1];
             fp1 = rw[R + 2];
-            if constexpr (R >= 3) need_next = __ballot((rw[R + 1] | rw[R + 2] | rw[R + 3] | rw[R + 4]) != 0u) != 0ull;
+            if constexpr (R >= 3)
+                need_next = need_next && __ballot((rw[R + 1] | rw[R + 2] | rw[R + 3] | rw[R + 4]) != 0u) != 0ull;
         }
         dring[5] = dflags(dnew);
         Dv1 += dring[4] - dring[1];

@@ -95,6 +95,14 @@ def main(prof_dir, tag, out_dir="profiles"):
             wr = sum(vals[s]["WRITE_SIZE"]) / len(vals[s]["WRITE_SIZE"]) * 1024
             traffic[s] = {"read_bytes": fe, "write_bytes": wr, "bytes_per_launch": fe + wr}
             lines.append(f"| {s} | HBM bytes (corrected) | {fe + wr:.6g} (read {fe:.4g}, write {wr:.4g}) |")
+        if "SQ_ACTIVE_INST_VALU" in vals[s] and "GRBM_GUI_ACTIVE" in vals[s]:
+            # SQ_ACTIVE_INST_VALU counts quad-cycles (a wave64 VALU op holds a 16-lane SIMD for 4 cycles);
+            # GRBM_GUI_ACTIVE is summed over the 8 XCDs: VALU-busy share of the 1024 SIMDs over the launch
+            va = sum(vals[s]["SQ_ACTIVE_INST_VALU"]) / len(vals[s]["SQ_ACTIVE_INST_VALU"])
+            gr = sum(vals[s]["GRBM_GUI_ACTIVE"]) / len(vals[s]["GRBM_GUI_ACTIVE"])
+            busy = va * 4 / (1024 * gr / 8)
+            traffic.setdefault(s, {})["valu_busy"] = busy
+            lines.append(f"| {s} | VALU busy (SQ_ACTIVE_INST_VALU x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)) | {busy:.3f} |")
     with open(os.path.join(out_dir, f"{tag}_summary.md"), "w") as f:
         f.write("\n".join(lines) + "\n")
     tj = os.path.join(out_dir, "pmc_traffic.json")

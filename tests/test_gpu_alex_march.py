@@ -165,3 +165,28 @@ def test_march_rejects_bad_shapes(device):
     with pytest.raises(GCAError):
         call("gca_alex_step_march", p, 1, 16, 512, dev.ptr(g), dev.ptr(g.clone()), dev.ptr(g), dev.ptr(g), dev.ptr(g),
              dev.ptr(g), dev.ptr(g), dev.ptr(g), None, None, None, None, dev.stream_ptr())
+
+
+def test_march_other_cell_codes(device):
+    """Arbitrary cell codes (FIRE = 0, EMPTY = 7, TREE = 3, plus cells of a fourth code the rule leaves alone): the
+    marching step equals the tiled one, including the EMPTY padding outside the grid (a FIRE code of 0 must not make
+    the border burn)."""
+    from alex_cases import winds
+    from gymca_amd.forest_fire.operators.ca_alexandridis import make_alex_params
+
+    E, H, W = 2, 48, 256
+    case = make_case(E, H, W, 71, p_tree=0.01, dousing_p=0.2, fire_p=0.05)
+    codes = np.array([7, 3, 0], np.uint8)
+    g = codes[case["grid"]]
+    g[:, 5, 10:20] = 9  # a code outside {empty, tree, fire}
+    case["grid"] = g
+    p, _ = make_alex_params(H, 7, 3, 0, winds(), 0.01, 99)
+    es, _ = slopes(device, altitude(E, H, W, 71))
+    coal = _coalesced(device, es)
+    vd, bits = _layers(device, case)
+    rs = np.full(E, 5, np.uint32)
+    g0, a0, c0, t0, _ = _run(device, "gca_alex_step_packed", p, case, coal, rs, vd, bits)
+    g1, a1, c1, t1, _ = _run(device, "gca_alex_step_march", p, case, es, rs, vd, bits)
+    assert np.array_equal(g1, g0), np.argwhere(g1 != g0)[:5]
+    assert np.array_equal(a1, a0) and np.array_equal(c1, c0) and np.array_equal(t1, t0)
+    assert (g1[:, 5, 10:20] == 9).all()
