@@ -312,12 +312,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
         }
         // Row r+2's slope planes (loaded during this row) serve rows r+1 and r+2, which can only need them with a FIRE
         // in rows r..r+3, and only inside the tile (the last row's row r+2 is the next tile's): otherwise the load
-        // re-reads row r+1's planes, which this wave loaded one row ago (an L2 hit, no HBM traffic; a branch around
-        // the load would keep SC live and cost registers), and the values are never used (those rows' row_need is
-        // false). The ring holds rows up to r+R; R < 3 always loads.
+        // re-reads the tile's first row, which every skipped load of the wave touches (L2-resident: no HBM traffic;
+        // a branch around the load would keep SC live and cost registers), and the values are never used (those
+        // rows' row_need is false). The ring holds rows up to r+R; R < 3 always loads.
         bool need_next = i + 1 < SH;
         auto load_next_slopes = [&]() {  // row r+2's raw planes into SC
-            const size_t rs = (size_t)min(need_next ? r + 2 : r + 1, H - 1);
+            const size_t rs = need_next ? (size_t)min(r + 2, H - 1) : (size_t)s0;
 #pragma unroll
             for (int k = 0; k < 4; ++k) SC[k] = ld_at<float4>(sE + (size_t)k * HW + rs * MW, lane_s);
         };
