@@ -58,7 +58,7 @@ __host__ __device__ constexpr bool win_full(int o, int j, int k) { return j - k 
 // B[j] = sum of the byte counts X over columns 4l+j-k .. 4l+j+k (k <= 8: lanes l-2 .. l+2), v_dot4_u32_u8 chains. The
 // dwords a window covers fully (always a run around the lane's own: {0}, {-1,0}, {0,1} or {-1,0,1} for k >= 2) are summed
 // once and shared by the four windows; the partial dwords are added with their byte masks (k = 6: 10 dot4 instead of 16)
-__device__ __forceinline__ void window4(uint32_t X, int k, uint32_t (&B)[4]) {
+__device__ __forceinline__ void window4(uint32_t X, int k, uint32_t (&B)[4], uint32_t z = 0u) {
     uint32_t n[5] = {0u, 0u, X, 0u, 0u};
     if (k >= 1) {
         n[1] = from_prev(X);
@@ -80,7 +80,7 @@ __device__ __forceinline__ void window4(uint32_t X, int k, uint32_t (&B)[4]) {
         else if (f0) use0 = true;
     }
     uint32_t S0 = 0u, SL = 0u, SR = 0u, SLR = 0u;
-    if (use0 || useL || useR || useLR) S0 = __builtin_amdgcn_udot4(n[2], ONES, 0u, false);
+    if (use0 || useL || useR || useLR) S0 = __builtin_amdgcn_udot4(n[2], ONES, z, false);
     if (useL || useLR) SL = __builtin_amdgcn_udot4(n[1], ONES, S0, false);
     if (useR) SR = __builtin_amdgcn_udot4(n[3], ONES, S0, false);
     if (useLR) SLR = __builtin_amdgcn_udot4(n[3], ONES, SL, false);
@@ -88,7 +88,7 @@ __device__ __forceinline__ void window4(uint32_t X, int k, uint32_t (&B)[4]) {
     for (int j = 0; j < 4; ++j) {
         const bool f0 = win_full(0, j, k), fl = win_full(-1, j, k), fr = win_full(1, j, k);
         const bool run = f0;  // the full dwords of a window with the lane's own are a run containing it
-        uint32_t acc = !run ? 0u : (fl && fr) ? SLR : fl ? SL : fr ? SR : S0;
+        uint32_t acc = !run ? z : (fl && fr) ? SLR : fl ? SL : fr ? SR : S0;
 #pragma unroll
         for (int o = -2; o <= 2; ++o) {
             if (run && (o == 0 || (o == -1 && fl) || (o == 1 && fr))) continue;  // inside the shared sum
@@ -104,13 +104,19 @@ __device__ __forceinline__ float4 ldf4(const float* p) { return *reinterpret_cas
 template <class T, class B> __device__ __forceinline__ T ld_at(const B* base, uint32_t off) {
     return *reinterpret_cast<const T*>(reinterpret_cast<const unsigned char*>(base) + off);
 }
+// Window sums as f32 pairs: the dot4 chains start from 2^23 (as f32 bits), so the sum's bits read as the float
+// 2^23 + B exactly (B < 2^23) and one packed subtract gives (float)B for two cells instead of a v_cvt_f32_u32 each
+constexpr uint32_t WZ = 0x4B000000u;
+__device__ __forceinline__ gca_f2 wsum_f2(uint32_t b0, uint32_t b1) {
+    return (gca_f2){__uint_as_float(b0), __uint_as_float(b1)} - (gca_f2){8388608.0f, 8388608.0f};
+}
 typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
 typedef int16_t i16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ i16x2 bitcast_i16x2(uint32_t v) { return __builtin_bit_cast(i16x2, v); }
 __device__ __forceinline__ u16x2 bitcast_u16x2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
 template <class T> __device__ __forceinline__ uint32_t bitcast_u32(T v) { return __builtin_bit_cast(uint32_t, v); }
 
-template <int R, bool OBS>
+template <int R, bool OBS, bool GROW>  // GROW: p_tree > 0 (EMPTY cells draw too)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void alex_march_kernel(
     gca_alex_params p, int H, int nwaves, const uint8_t* __restrict__ grid_in, uint8_t* __restrict__ grid_out,
     const int16_t* age_in, int16_t* age_out,  // no __restrict__: the env updates ages in place
@@ -276,11 +282,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
 #pragma unroll
     for (int k = 0; k < 3; ++k) prep_own(sc[k]);
 
-    float wind[8];
+    // the per-env constants of the packed f32 arithmetic as (x, x) pairs held in VGPRs: as SGPR operands hipcc
+    // materialises every pair as two SGPRs, and the 30-odd of them were spilled to VGPR lanes and read back per row
+    gca_f2 wind2[8], hdw2[R + 1];
     {
         const int widx = wind_index[e];
 #pragma unroll
-        for (int d = 0; d < 8; ++d) wind[d] = p.winds[widx][d < 4 ? d : d + 1];
+        for (int d = 0; d < 8; ++d) {
+            const float w = p.winds[widx][d < 4 ? d : d + 1];
+            wind2[d] = (gca_f2){w, w};
+            asm volatile("" : "+v"(wind2[d]));
+        }
+#pragma unroll
+        for (int k = 0; k <= R; ++k) {
+            hdw2[k] = (gca_f2){p.heat_dw[k], p.heat_dw[k]};
+            asm volatile("" : "+v"(hdw2[k]));
+        }
     }
     const uint32_t step = rng_step ? rng_step[e] : 0u;
     const uint32_t k0 = (uint32_t)p.seed, k1 = (uint32_t)(p.seed >> 32);
@@ -299,16 +316,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
         //      loads are unused, and unconditional loads keep the two rows of the loop body branch-free)
         const uint32_t gnew = nG, dnew = nD, own = nOwn, vdw = nVD;
         const uint2 agep = nAge;
-        {  // (wave-uniform row base pointers + a 32-bit lane byte offset: SGPR-based addressing, no 64-bit VALU math)
+        {  // (wave-uniform row base pointers + a 32-bit lane byte offset; raw buffer loads with SGPR row offsets were
+           //  measured 2.5 % slower, profiles/r03n/ab_buffer_loads.txt)
             const int rg = r + 1 + R, rd = r + 3;
-            const size_t r1 = (size_t)min(r + 1, H - 1);
+            const uint32_t r1 = (uint32_t)min(r + 1, H - 1);
             const uint32_t g = ld_at<uint32_t>(gE + (size_t)min(rg, H - 1) * MW, lc);
             const uint32_t d = ld_at<uint16_t>(dE + (size_t)min(rd, H - 1) * (MW / 16), lane_d);
+            nOwn = ld_at<uint32_t>(gE + (size_t)r1 * MW, lc);
+            nVD = ld_at<uint32_t>(vE + (size_t)r1 * MW, lc);
+            nAge = ld_at<uint2>(aE + (size_t)r1 * MW, lane_a);
             nG = rg < H ? g : Ep;
             nD = rd < H ? d : 0u;
-            nOwn = ld_at<uint32_t>(gE + r1 * MW, lc);
-            nVD = ld_at<uint32_t>(vE + r1 * MW, lc);
-            nAge = ld_at<uint2>(aE + r1 * MW, lane_a);
         }
         // Row r+2's slope planes (loaded during this row) serve rows r+1 and r+2, which can only need them with a FIRE
         // in rows r..r+3, and only inside the tile (the last row's row r+2 is the next tile's): otherwise the load
@@ -317,9 +335,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
         // rows' row_need is false). The ring holds rows up to r+R; R < 3 always loads.
         bool need_next = i + 1 < SH;
         auto load_next_slopes = [&]() {  // row r+2's raw planes into SC
-            const size_t rs = need_next ? (size_t)min(r + 2, H - 1) : (size_t)s0;
+            const uint32_t rs = need_next ? (uint32_t)min(r + 2, H - 1) : (uint32_t)s0;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) SC[k] = ld_at<float4>(sE + (size_t)k * HW + rs * MW, lane_s);
+            for (int k = 0; k < 4; ++k) SC[k] = ld_at<float4>(sE + (size_t)k * HW + (size_t)rs * MW, lane_s);
         };
         // ---- fire ring: row r+R enters; the running vertical sums move to row r
         const int t0 = i % NF;  // slot of row r-R-1
@@ -400,24 +418,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
 #pragma unroll
                     for (int j = 0; j < 4; ++j) B[j] = (f0 >> (8 * j)) & 0xFFu;
                 } else {
-                    window4(V[k], k, B);
+                    window4(V[k], k, B, WZ);
                 }
-                const float wk = p.heat_dw[k];
 #pragma unroll
                 for (int h = 0; h < 2; ++h)
-                    ph[h] = __builtin_elementwise_fma((gca_f2){wk, wk}, (gca_f2){(float)B[2 * h], (float)B[2 * h + 1]}, ph[h]);
+                    ph[h] = __builtin_elementwise_fma(hdw2[k], k == 0 ? (gca_f2){(float)B[2 * h], (float)B[2 * h + 1]}
+                                                                       : wsum_f2(B[2 * h], B[2 * h + 1]), ph[h]);
                 // one radius at a time (hipcc would otherwise interleave all the radii's DPP / dot4 work)
                 asm volatile("" : "+v"(ph[0]), "+v"(ph[1]));
                 __builtin_amdgcn_sched_barrier(0);
             }
             uint32_t D1[4], D2[4];
-            window4(Dv1, 1, D1);
-            window4(Dv2, 2, D2);
+            window4(Dv1, 1, D1, WZ);
+            window4(Dv2, 2, D2, WZ);
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-                gca_f2 dz = (gca_f2){w_in_minus_bd, w_in_minus_bd} * (gca_f2){(float)D1[2 * h], (float)D1[2 * h + 1]};
-                dz = __builtin_elementwise_fma((gca_f2){p.dous_border, p.dous_border},
-                                               (gca_f2){(float)D2[2 * h], (float)D2[2 * h + 1]}, dz);
+                gca_f2 dz = (gca_f2){w_in_minus_bd, w_in_minus_bd} * wsum_f2(D1[2 * h], D1[2 * h + 1]);
+                dz = __builtin_elementwise_fma((gca_f2){p.dous_border, p.dous_border}, wsum_f2(D2[2 * h], D2[2 * h + 1]), dz);
                 ph[h] = ph[h] - dz;
             }
             // ---- base = (p_h * (1 + p_veg)) * (1 + p_den)
@@ -437,7 +454,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
                     // pin base and the product: otherwise the direction-independent work of all 8 directions is
                     // hoisted (as in gca_alex.hip)
                     asm volatile("" : "+v"(ph[0]), "+v"(ph[1]), "+v"(qn[0]), "+v"(qn[1]));
-                    const gca_f2 wd2 = {wind[d], wind[d]};
+                    const gca_f2 wd2 = wind2[d];
                     const uint32_t Md = dir_mask(d);
 #pragma unroll
                     for (int h = 0; h < 2; ++h) {
@@ -515,25 +532,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
         }
 
         // ---- draws: one Philox block per cell pair (cells 4l, 4l+1 and 4l+2, 4l+3), as gca_alex.hip
-        const uint32_t needB = (treeB & anyfire) | (p.p_tree > 0.0f ? emptyB : 0u);
+        const uint32_t needB = (treeB & anyfire) | (GROW ? emptyB : 0u);
         const uint32_t lin0 = (uint32_t)r * MW + lc;
         uint32_t burn = 0u, grow = 0u, NA[2];
         // every lane draws when any lane of the wave needs to (a wave-uniform branch instead of a masked one per
         // pair): the draws of cells that need none are discarded (qn = 1 gives thr = 0; grow is masked by EMPTY)
         const bool wave_draws = __ballot(needB != 0u) != 0ull;
+        // the Philox round keys are rebuilt per row by s_add (hoisted, the 20 of them were spilled to VGPR lanes
+        // and read back per row)
+        uint32_t rk0 = k0, rk1 = k1;
+        asm volatile("" : "+s"(rk0), "+s"(rk1));
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             u32x4 X = u32x4{0u, 0u, 0u, 0u};
             if (wave_draws)
-                X = philox4x32_10(u32x4{(lin0 >> 1) + (uint32_t)h, env_id, step, GCA_TAG_ALEX_CELL}, k0, k1);
+                X = philox4x32_10(u32x4{(lin0 >> 1) + (uint32_t)h, env_id, step, GCA_TAG_ALEX_CELL}, rk0, rk1);
             // thr = fl(1 - qn) * 2^24 = fl(2^24 - qn * 2^24) (power-of-two scaling commutes with the rounding)
             const gca_f2 thr = __builtin_elementwise_fma(qn[h], (gca_f2){-16777216.0f, -16777216.0f},
                                                          (gca_f2){16777216.0f, 16777216.0f});
             const float u0 = (float)(X.x >> 8), u1 = (float)(X.z >> 8);
             burn |= (u0 < thr.x ? 1u : 0u) << (2 * h);
             burn |= (u1 < thr.y ? 1u : 0u) << (2 * h + 1);
-            grow |= (u0 < pt24 ? 1u : 0u) << (2 * h);
-            grow |= (u1 < pt24 ? 1u : 0u) << (2 * h + 1);
+            if constexpr (GROW) {
+                grow |= (u0 < pt24 ? 1u : 0u) << (2 * h);
+                grow |= (u1 < pt24 ? 1u : 0u) << (2 * h + 1);
+            }
             const uint32_t n0 = (uint32_t)randint_ms(X.y, p.age_lo, p.age_hi);
             const uint32_t n1 = (uint32_t)randint_ms(X.w, p.age_lo, p.age_hi);
             NA[h] = __builtin_amdgcn_perm(n1, n0, 0x05040100u);
@@ -607,14 +630,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     }
 }
 
+template <int R, bool OBS, bool GROW>
+void launch_march_g(const gca_alex_params& p, int E, int H, const uint8_t* gi, uint8_t* go, const int16_t* ai,
+                  int16_t* ao, const uint8_t* vd, const uint16_t* db, const float* es, const int32_t* wi,
+                  const uint32_t* rs, int32_t* counts, const uint8_t* act_in, uint8_t* act_out, MarchObs obs,
+                  hipStream_t st) {
+    const int nwaves = E * (H / SH);
+    hipLaunchKernelGGL((alex_march_kernel<R, OBS, GROW>), dim3((unsigned)((nwaves + 3) / 4)), dim3(256), 0, st, p, H, nwaves,
+                       gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs);
+}
 template <int R, bool OBS>
 void launch_march(const gca_alex_params& p, int E, int H, const uint8_t* gi, uint8_t* go, const int16_t* ai,
                   int16_t* ao, const uint8_t* vd, const uint16_t* db, const float* es, const int32_t* wi,
                   const uint32_t* rs, int32_t* counts, const uint8_t* act_in, uint8_t* act_out, MarchObs obs,
                   hipStream_t st) {
-    const int nwaves = E * (H / SH);
-    hipLaunchKernelGGL((alex_march_kernel<R, OBS>), dim3((unsigned)((nwaves + 3) / 4)), dim3(256), 0, st, p, H, nwaves,
-                       gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs);
+    if (p.p_tree > 0.0f)
+        launch_march_g<R, OBS, true>(p, E, H, gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs, st);
+    else
+        launch_march_g<R, OBS, false>(p, E, H, gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs, st);
 }
 
 template <bool OBS>

@@ -10,7 +10,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "gym-cellular-automata_amd")]
 
 
-def main(E=4096, N=256, K=10, reps=5, hidden=False):
+def main(E=4096, N=256, K=10, reps=5, hidden=False, only=None, rgb_modes=(False, True)):
     import torch
 
     import bench
@@ -41,8 +41,10 @@ def main(E=4096, N=256, K=10, reps=5, hidden=False):
         env.cur = b
 
     out = {"E": E, "N": N, "K": K, "reps": reps, "hidden": hidden}
-    for rgb in (False, True):
+    for rgb in rgb_modes:
         for fn in ("gca_alex_step_packed", "gca_alex_step_march"):
+            if only and only not in fn:
+                continue
             times = []
             for _ in range(reps):
                 bench.synthetic_state(env, 0, device)
@@ -61,4 +63,8 @@ def main(E=4096, N=256, K=10, reps=5, hidden=False):
 
 
 if __name__ == "__main__":
-    main(hidden="--hidden" in sys.argv)
+    # --only march|packed: one mapping; --plain: no fused-frame variants; --reps N
+    args = sys.argv[1:]
+    only = args[args.index("--only") + 1] if "--only" in args else None
+    reps = int(args[args.index("--reps") + 1]) if "--reps" in args else 5
+    main(hidden="--hidden" in args, only=only, reps=reps, rgb_modes=(False,) if "--plain" in args else (False, True))
