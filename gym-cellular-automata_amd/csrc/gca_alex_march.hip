@@ -139,7 +139,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     const int wv = lb * 4 + wl;
     if (wv >= nwaves) return;  // wave-uniform; no barrier follows
     const int strips = H / SH;
-    const int e = wv / strips, s = wv - e * strips, s0 = s * SH;
+    // (env-major wave order: one env's tiles back to back. A tile-major order inside chunks of 128 / 256 / 512 envs,
+    //  meant to turn the tiles' shared halo rows into L2 hits, measured 5 / 8 / 12 % slower, profiles/r03p)
+    const int e = wv / strips, s = wv - e * strips;
+    const int s0 = s * SH;
     const uint32_t HW = (uint32_t)H * MW;
     const uint8_t* gE = grid_in + (size_t)e * HW;
     uint8_t* gO = grid_out + (size_t)e * HW;
@@ -173,13 +176,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     auto write_rgb_row = [&](int r, uint32_t tB, uint32_t fB, uint32_t dfl) {
         if constexpr (OBS) {
             const uint32_t kidx = 2u * gca_spread4(tB) + 4u * gca_spread4(fB) + (dfl & 0x01010101u);
-            float4 c[4];
+            // one cell at a time (3 live VGPRs instead of the 16 of four colours: the frame is written at the end of
+            // the row, where row r+1's loads are in flight and the register file is full)
+            float* im = reinterpret_cast<float*>(img[wl]) + 12 * lane;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) c[j] = colw[wl][(kidx >> (8 * j)) & 0xFFu];
-            float4* im = img[wl] + 3 * lane;
-            im[0] = make_float4(c[0].x, c[0].y, c[0].z, c[1].x);
-            im[1] = make_float4(c[1].y, c[1].z, c[2].x, c[2].y);
-            im[2] = make_float4(c[2].z, c[3].x, c[3].y, c[3].z);
+            for (int j = 0; j < 4; ++j) {
+                const float4 c = colw[wl][(kidx >> (8 * j)) & 0xFFu];
+                im[3 * j + 0] = c.x;
+                im[3 * j + 1] = c.y;
+                im[3 * j + 2] = c.z;
+            }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -236,10 +242,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
 
     // ---- fire ring in LDS: the FIRE flags (0x01 bytes) of rows r-R-1 .. r+R, one dword per lane and row, each row
     //      stored twice (slots t and t + NF), so that the rows around r sit at fixed offsets from one base that moves
-    //      by one slot per row: immediate-offset ds_read_b32, no register rotation
+    //      by one slot per row: immediate-offset ds_read_b32, no register rotation. Rows are stored in DESCENDING
+    //      order (the base moves down one slot per row): the entering row sits at the base and its copy at base + NF,
+    //      both immediate offsets off the address the reads use (ascending order put the copy at base - 1, which took
+    //      a second per-lane address register and, in the fused-frame variant, a spill, r03p)
     uint32_t* FR = fring[wl];
-    auto ring_put = [&](int t, uint32_t v) {  // relative row t = row - (s0 - R - 1)
-        const int sl = t % NF;
+    auto ring_put = [&](int t, uint32_t v) {  // relative row t = row - (s0 - R - 1): slot NF - 1 - t (row 0's base)
+        const int sl = (2 * NF - 2 - t) % NF;
         FR[sl * 64 + lane] = v;
         FR[(sl + NF) * 64 + lane] = v;
     };
@@ -249,6 +258,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
 #pragma unroll
     for (int t = 0; t < 5; ++t) dring[t] = dflags(draw_bits(s0 - 3 + t));
     // loads of row s0 (and the slopes of rows s0, s0+1)
+    // row r's own codes are re-read one row ahead (nOwn) although the ring saw them R rows earlier: a per-wave LDS ring
+    // of the codes instead cuts the traffic by 1.0 B / cell (26.2 -> 25.2) but measured 0.6-2 % slower (r03q/r03r)
     uint32_t nG = graw(s0 + R), nD = draw_bits(s0 + 2), nOwn = graw(s0);
     uint32_t nVD = *reinterpret_cast<const uint32_t*>(vE + (size_t)s0 * MW + lc);
     uint2 nAge = *reinterpret_cast<const uint2*>(aE + (size_t)s0 * MW + lc);
@@ -266,7 +277,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     for (int k = 1; k <= R; ++k) {
         uint32_t v = 0u;
 #pragma unroll
-        for (int t = R - k; t <= R + k; ++t) v += FR[t * 64 + lane];
+        for (int t = R - k; t <= R + k; ++t) v += FR[((2 * NF - 2 - t) % NF) * 64 + lane];
         V[k] = v;
     }
     uint32_t Dv1 = dring[1] + dring[2] + dring[3];
@@ -282,23 +293,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
 #pragma unroll
     for (int k = 0; k < 3; ++k) prep_own(sc[k]);
 
-    // the per-env constants of the packed f32 arithmetic as (x, x) pairs held in VGPRs: as SGPR operands hipcc
-    // materialises every pair as two SGPRs, and the 30-odd of them were spilled to VGPR lanes and read back per row
-    gca_f2 wind2[8], hdw2[R + 1];
+    // the per-env constants of the packed f32 arithmetic, two per VGPR pair, held in VGPRs: as SGPR operands hipcc
+    // materialises every (x, x) pair as two SGPRs, and the 30-odd of them were spilled to VGPR lanes and read back per
+    // row. A constant is used as the pair (x, x) through op_sel (one half of the pair broadcast), so the 8 winds and
+    // R + 1 heat weights take 8 + 2 ceil((R + 1) / 2) VGPRs instead of 16 + 2 (R + 1) (r03p: the fused-frame variant
+    // spilled two VGPRs, whose per-row reloads waited for the row-ahead loads)
+    constexpr int NHW = (R + 2) / 2;
+    gca_f2 windp[4], hdwp[NHW];
     {
         const int widx = wind_index[e];
 #pragma unroll
-        for (int d = 0; d < 8; ++d) {
-            const float w = p.winds[widx][d < 4 ? d : d + 1];
-            wind2[d] = (gca_f2){w, w};
-            asm volatile("" : "+v"(wind2[d]));
+        for (int q = 0; q < 4; ++q) {
+            const int d0 = 2 * q, d1 = 2 * q + 1;
+            windp[q] = (gca_f2){p.winds[widx][d0 < 4 ? d0 : d0 + 1], p.winds[widx][d1 < 4 ? d1 : d1 + 1]};
+            asm volatile("" : "+v"(windp[q]));
         }
 #pragma unroll
-        for (int k = 0; k <= R; ++k) {
-            hdw2[k] = (gca_f2){p.heat_dw[k], p.heat_dw[k]};
-            asm volatile("" : "+v"(hdw2[k]));
+        for (int q = 0; q < NHW; ++q) {
+            hdwp[q] = (gca_f2){p.heat_dw[2 * q], 2 * q + 1 <= R ? p.heat_dw[2 * q + 1] : 0.0f};
+            asm volatile("" : "+v"(hdwp[q]));
         }
     }
+    auto bcast = [](gca_f2 v, int h) -> gca_f2 {
+        return h ? __builtin_shufflevector(v, v, 1, 1) : __builtin_shufflevector(v, v, 0, 0);
+    };
     const uint32_t step = rng_step ? rng_step[e] : 0u;
     const uint32_t k0 = (uint32_t)p.seed, k1 = (uint32_t)(p.seed >> 32);
     const uint32_t env_id = (uint32_t)(p.env_offset + e);
@@ -336,16 +354,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
         bool need_next = i + 1 < SH;
         auto load_next_slopes = [&]() {  // row r+2's raw planes into SC
             const uint32_t rs = need_next ? (uint32_t)min(r + 2, H - 1) : (uint32_t)s0;
+            // plane 3 of row r+2 serves row r+2 itself only: the next tile's first row (i = SH - 2) skips it too
+            const uint32_t rs3 = i + 2 < SH ? rs : (uint32_t)s0;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) SC[k] = ld_at<float4>(sE + (size_t)k * HW + (size_t)rs * MW, lane_s);
+            for (int k = 0; k < 4; ++k)
+                SC[k] = ld_at<float4>(sE + (size_t)k * HW + (size_t)(k == 3 ? rs3 : rs) * MW, lane_s);
         };
         // ---- fire ring: row r+R enters; the running vertical sums move to row r
-        const int t0 = i % NF;  // slot of row r-R-1
-        uint32_t* Fb = FR + t0 * 64;
+        uint32_t* Fb = FR + (NF - 1 - (uint32_t)i % NF) * 64;  // slot of row r+R; row r+R-t at slot + t
         {
-            const uint32_t fnew = bytes_eq01(gnew, Fp);
-            Fb[(NF - 1) * 64 + lane] = fnew;
-            Fb[(t0 == 0 ? 2 * NF - 1 : -1) * 64 + lane] = fnew;
+            const uint32_t fnew = bytes_eq01(gnew, Fp);  // row r+R: offset 0 and its copy at +NF (both immediates off
+            Fb[lane] = fnew;                             // the one address the reads use)
+            Fb[NF * 64 + lane] = fnew;
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -354,7 +374,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
         {
             uint32_t rw[NF];
 #pragma unroll
-            for (int t = 0; t < NF; ++t) rw[t] = Fb[t * 64 + lane];
+            for (int t = 0; t < NF; ++t) rw[t] = Fb[(NF - 1 - t) * 64 + lane];  // rw[t] = row r-R-1+t
 #pragma unroll
             for (int k = 1; k <= R; ++k) V[k] += rw[R + 1 + k] - rw[R - k];
             fm1 = rw[R];
@@ -422,7 +442,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
                 }
 #pragma unroll
                 for (int h = 0; h < 2; ++h)
-                    ph[h] = __builtin_elementwise_fma(hdw2[k], k == 0 ? (gca_f2){(float)B[2 * h], (float)B[2 * h + 1]}
+                    ph[h] = __builtin_elementwise_fma(bcast(hdwp[k >> 1], k & 1), k == 0 ? (gca_f2){(float)B[2 * h], (float)B[2 * h + 1]}
                                                                        : wsum_f2(B[2 * h], B[2 * h + 1]), ph[h]);
                 // one radius at a time (hipcc would otherwise interleave all the radii's DPP / dot4 work)
                 asm volatile("" : "+v"(ph[0]), "+v"(ph[1]));
@@ -454,7 +474,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
                     // pin base and the product: otherwise the direction-independent work of all 8 directions is
                     // hoisted (as in gca_alex.hip)
                     asm volatile("" : "+v"(ph[0]), "+v"(ph[1]), "+v"(qn[0]), "+v"(qn[1]));
-                    const gca_f2 wd2 = wind2[d];
+                    const gca_f2 wd2 = bcast(windp[d >> 1], d & 1);
                     const uint32_t Md = dir_mask(d);
 #pragma unroll
                     for (int h = 0; h < 2; ++h) {
