@@ -473,7 +473,9 @@ def bench_windy(args, world, rank, device, pg):
         "config": "ForestFireBulldozer 256x256, 1024 envs/GPU, WindyForestFire",
         "env_steps_per_s": world * E * Kg * G / dt_env,
         "env_steps_per_s_eager": world * E * K / dt_eager,
-        "env_step_graph": f"hipGraph of {G} env steps (random actions + RepeatCA/Windy passes + Move/Modify + reward)",
+        "env_step_graph": f"hipGraph of {G} env steps (random actions + " + (
+            "gca_bulldozer_step_fused: RepeatCA, Windy CA, Move/Modify and reward in one launch)" if env.fused else
+            "RepeatCA/Windy passes + Move/Modify + reward)"),
         "ca_only_cell_updates_per_s": world * E * N * N * K / dt_ca,
         "ca_kernel_ms": kern * 1e3,
         "ca_achieved_gbs": WINDY_BYTES_PER_CELL * E * N * N / kern / 1e9,
@@ -539,6 +541,8 @@ def bench_windy512(args, world, rank, device, pg):
     ca = windy_ca_only(env, K, args.warmup, pg, device)
     return {"config": "ForestFireBulldozer 512x512, 1024 envs/GPU (BASELINE config 5 at 8 GPUs), WindyForestFire",
             "env_steps_per_s": world * E * Kg * G / dt_g,
+            "env_step": ("gca_bulldozer_step_fused (one launch per env step)" if env.fused else
+                         "pre / Windy passes / post kernels"),
             "env_steps_per_s_eager_gather_every_step": world * E * K / dt_eager,
             "env_steps_per_s_async_gather_every_step": world * E * K / dt_async,
             "gather": ("RCCL all_gather_into_tensor of reward f32 | length | done u8 per env into a reused buffer "

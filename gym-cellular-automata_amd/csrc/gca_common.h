@@ -70,6 +70,22 @@ __device__ __forceinline__ int32_t randint_ms(uint32_t x, int32_t lo, int32_t hi
     return lo + (int32_t)__umulhi(x, span);
 }
 
+// ----------------------------------------------------------------- env helpers (gca_env.hip, gca_windy.hip)
+__device__ __forceinline__ int clampi_dev(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+// Move.update (move_modify.py:37-67): the four set tests run in order on the running (row, col).
+__device__ __forceinline__ void move_pos(int a, int& row, int& col, int H, int W, int up, int down, int left,
+                                         int right) {
+    const bool valid_up = row > 0, valid_down = row < H - 1, valid_left = col > 0, valid_right = col < W - 1;
+    if (((up >> a) & 1) && valid_up) row -= 1;
+    if (((down >> a) & 1) && valid_down) row += 1;
+    if (((left >> a) & 1) && valid_left) col -= 1;
+    if (((right >> a) & 1) && valid_right) col += 1;
+}
+// count slot of a cell code: 0 EMPTY, 1 TREE, 2 FIRE, -1 other
+__device__ __forceinline__ int cell_category(int v, int empty, int tree, int fire) {
+    return v == empty ? 0 : (v == tree ? 1 : (v == fire ? 2 : -1));
+}
+
 // WindyForestFire active-direction mask (ca_windy.py:53-77): bit d set iff roll[d] < wind[d]
 // (the reference marks d as failed iff wind <= roll). d indexes the 3x3 row-major, centre skipped.
 __device__ __forceinline__ uint32_t windy_mask(const double* __restrict__ w, const double* __restrict__ roll,

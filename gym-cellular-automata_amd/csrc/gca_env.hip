@@ -8,21 +8,8 @@
 
 #include "gca_common.h"
 
-__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
-
-// Move.update (move_modify.py:37-67): the four set tests run in order on the running (row, col).
-__device__ __forceinline__ void move_pos(int a, int& row, int& col, int H, int W, int up, int down, int left,
-                                         int right) {
-    const bool valid_up = row > 0, valid_down = row < H - 1, valid_left = col > 0, valid_right = col < W - 1;
-    if (((up >> a) & 1) && valid_up) row -= 1;
-    if (((down >> a) & 1) && valid_down) row += 1;
-    if (((left >> a) & 1) && valid_left) col -= 1;
-    if (((right >> a) & 1) && valid_right) col += 1;
-}
-
-__device__ __forceinline__ int category(int v, int empty, int tree, int fire) {
-    return v == empty ? 0 : (v == tree ? 1 : (v == fire ? 2 : -1));
-}
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return clampi_dev(v, lo, hi); }
+__device__ __forceinline__ int category(int v, int empty, int tree, int fire) { return cell_category(v, empty, tree, fire); }
 
 // ================================================================== ForestFireBulldozer
 __global__ void bulldozer_pre_kernel(gca_bulldozer_params p, const int32_t* __restrict__ action,

@@ -316,30 +316,16 @@ __device__ __forceinline__ RowCls<NW> classify_row(const RowRaw<NW>& x, bool val
     return o;
 }
 
-template <int NW>
-__global__ __launch_bounds__(256) void windy_rows_kernel(uint8_t* __restrict__ buf0, uint8_t* __restrict__ buf1,
-                                                         const uint8_t* __restrict__ parity,
-                                                         const int32_t* __restrict__ steps, int pass,
-                                                         const uint8_t* __restrict__ dir_mask, int H,
-                                                         int blocks_per_env, uint32_t Ep, uint32_t Tp, uint32_t Fp,
-                                                         int32_t* __restrict__ counts) {
+// One wave's strip of SH rows [s0, s0 + SH) of one env: S the input grid, Dst the output, m the env's direction mask;
+// the strip's new-grid counts are added to (cntT, cntF, cntV = cells written). Shared by windy_rows_kernel (one
+// launch per CA pass) and bulldozer_step_fused_kernel (the whole env step), so both write the same bytes. RD: rows of
+// loads in flight ahead of the row being classified (RD = SH: the whole strip at once), SH: the strip's height.
+template <int NW, int SH, int RD>
+__device__ __forceinline__ void windy_rows_strip(const uint8_t* __restrict__ S, uint8_t* __restrict__ Dst, int s0,
+                                                 int H, uint32_t m, uint32_t lofs, uint32_t Ep, uint32_t Tp,
+                                                 uint32_t Fp, int32_t& cntT, int32_t& cntF, int32_t& cntV) {
     constexpr int W = 256 * NW;
-    constexpr int SH = GCA_WINDY_RSH;
-    constexpr int RD = GCA_WINDY_RD;
-    const int env = blockIdx.x / blocks_per_env;
-    const int sblk = blockIdx.x - env * blocks_per_env;
-    if (steps && steps[env] <= pass) return;
-    // the wave index is wave-uniform: readfirstlane keeps s0 and every row index in SGPRs
-    const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const int s0 = (sblk * 4 + wave) * SH;
-    if (s0 >= H) return;
-    const bool odd = parity && parity[env];
-    const int64_t HW = (int64_t)H * W;
-    const uint8_t* __restrict__ S = (odd ? buf1 : buf0) + (int64_t)env * HW;
-    uint8_t* __restrict__ Dst = (odd ? buf0 : buf1) + (int64_t)env * HW;
-    const uint32_t lofs = 4 * NW * (uint32_t)lane;
-    // the env's direction mask, forced into an SGPR (a VGPR copy made hipcc rebuild some masks per row)
-    const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane((int)dir_mask[env]);
+    static_assert(RD >= 1 && RD <= SH, "rows in flight: 1 .. SH");
     // all-ones / zero per direction, made opaque (readfirstlane) so that hipcc keeps `(x & m) | acc` as one
     // v_and_or_b32 per direction instead of turning each mask into a v_cndmask plus a separate or
     auto dm = [&](uint32_t bit) {
@@ -359,7 +345,6 @@ __global__ __launch_bounds__(256) void windy_rows_kernel(uint8_t* __restrict__ b
     RowCls<NW> A = classify_row<NW>(r_up, s0 >= 1, Tp, Fp);
     RowCls<NW> B = classify_row<NW>(r_cur, true, Tp, Fp);
 
-    int32_t cntT = 0, cntF = 0, cntV = 0;
 #pragma unroll
     for (int t = 0; t < SH; ++t) {
         const int Rc = s0 + t;
@@ -401,6 +386,32 @@ __global__ __launch_bounds__(256) void windy_rows_kernel(uint8_t* __restrict__ b
         A = B;
         B = C;
     }
+}
+
+template <int NW>
+__global__ __launch_bounds__(256) void windy_rows_kernel(uint8_t* __restrict__ buf0, uint8_t* __restrict__ buf1,
+                                                         const uint8_t* __restrict__ parity,
+                                                         const int32_t* __restrict__ steps, int pass,
+                                                         const uint8_t* __restrict__ dir_mask, int H,
+                                                         int blocks_per_env, uint32_t Ep, uint32_t Tp, uint32_t Fp,
+                                                         int32_t* __restrict__ counts) {
+    constexpr int W = 256 * NW;
+    const int env = blockIdx.x / blocks_per_env;
+    const int sblk = blockIdx.x - env * blocks_per_env;
+    if (steps && steps[env] <= pass) return;
+    // the wave index is wave-uniform: readfirstlane keeps s0 and every row index in SGPRs
+    const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int s0 = (sblk * 4 + wave) * GCA_WINDY_RSH;
+    if (s0 >= H) return;
+    const bool odd = parity && parity[env];
+    const int64_t HW = (int64_t)H * W;
+    const uint8_t* __restrict__ S = (odd ? buf1 : buf0) + (int64_t)env * HW;
+    uint8_t* __restrict__ Dst = (odd ? buf0 : buf1) + (int64_t)env * HW;
+    const uint32_t lofs = 4 * NW * (uint32_t)lane;
+    // the env's direction mask, forced into an SGPR (a VGPR copy made hipcc rebuild some masks per row)
+    const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane((int)dir_mask[env]);
+    int32_t cntT = 0, cntF = 0, cntV = 0;
+    windy_rows_strip<NW, GCA_WINDY_RSH, GCA_WINDY_RD>(S, Dst, s0, H, m, lofs, Ep, Tp, Fp, cntT, cntF, cntV);
     if (counts) {
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) {
@@ -414,6 +425,113 @@ __global__ __launch_bounds__(256) void windy_rows_kernel(uint8_t* __restrict__ b
             atomicAdd(counts + 3 * env + 2, cntF);
         }
     }
+}
+
+// ------------------------------------------------------------------ the whole ForestFireBulldozer env step, fused
+template <int NW> constexpr int FUSED_SH = NW == 1 ? 16 : 32;  // strip height per wave of the fused step
+// One workgroup per env runs bulldozer.py's MDP.update (:393-400) for that env in one launch: RepeatCA's time
+// bookkeeping (repeat_ca.py:32-45), when a CA step is due the Windy direction mask (ca_windy.py:53-77) and the CA over
+// the env's grid (one wave per 16-row strip, windy_rows_strip: the same bytes as gca_windy_step), then Move / Modify
+// (move_modify.py:128-134) on the new grid and reward / done (bulldozer.py:180-216) from the fused counts. The
+// arithmetic is that of gca_bulldozer_pre / gca_windy_step / gca_bulldozer_post (one CA pass per env step at most,
+// host-checked), so the two paths give identical envs; the multi-kernel path launches four kernels per env step over
+// every env although only ~1 env in 13 takes a CA step, this one launch, and envs without a CA step
+// leave after their O(1) work.
+template <int NW>
+__global__ __launch_bounds__(1024) void bulldozer_step_fused_kernel(
+    gca_bulldozer_params p, const int32_t* __restrict__ action, double* __restrict__ accu, int32_t* __restrict__ steps,
+    uint8_t* __restrict__ done, const double* __restrict__ wind, int64_t wind_stride, uint32_t* __restrict__ rng_step,
+    uint8_t* __restrict__ parity, uint8_t* __restrict__ buf0, uint8_t* __restrict__ buf1, int H,
+    int32_t* __restrict__ pos, int32_t* __restrict__ counts, uint8_t* __restrict__ hit, double* __restrict__ reward,
+    int64_t* __restrict__ steps_elapsed) {
+    constexpr int W = 256 * NW;
+    constexpr int FSH = FUSED_SH<NW>;
+    __shared__ int32_t blk_cnt[3];
+    __shared__ uint32_t blk_mask;
+    const int e = blockIdx.x;
+    const int tid = threadIdx.x;
+    // ---- RepeatCA bookkeeping (every thread computes n from the same loads; thread 0 writes after the CA)
+    const bool was_done = done[e] != 0;
+    const int a0 = clampi_dev(action[2 * e], 0, 8), a1s = clampi_dev(action[2 * e + 1], 0, 1);
+    const double x = accu[e] + ((p.t_move[a0] + p.t_shoot[a1s]) + p.t_any);
+    const double reps = trunc(x);  // math.modf
+    const int n = was_done ? -1 : (int)reps;
+    const bool odd = parity[e] != 0;
+    const int64_t HW = (int64_t)H * W;
+    uint8_t* grid = (odd ? buf1 : buf0) + e * HW;  // the env's grid after this step
+    if (n > 0) {
+        if (tid == 0) {
+            blk_mask = windy_mask(wind + (int64_t)e * wind_stride, nullptr, (uint32_t)p.seed, (uint32_t)(p.seed >> 32),
+                                  (uint32_t)(p.env_offset + e), rng_step[e]);
+            blk_cnt[0] = blk_cnt[1] = blk_cnt[2] = 0;
+        }
+        __syncthreads();
+        const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, nw = (int)(blockDim.x >> 6);
+        const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane((int)blk_mask);
+        const uint8_t* __restrict__ S = grid;
+        uint8_t* __restrict__ Dst = (odd ? buf0 : buf1) + e * HW;
+        const uint32_t lofs = 4 * NW * (uint32_t)lane;
+        int32_t cntT = 0, cntF = 0, cntV = 0;
+        // strips of FSH rows with the whole strip's rows in flight at once: only the ~1 env in 13 (256^2; 1 in 25 at
+        // 512^2) with a CA step this env step runs here, so the launch is latency-bound, not occupancy-bound, and a
+        // wave's strip costs one round trip to memory (16 waves cover a 512-row grid in one strip each)
+        for (int s0 = wave * FSH; s0 < H; s0 += nw * FSH)
+            windy_rows_strip<NW, FSH, FSH>(S, Dst, s0, H, m, lofs, rep4(p.empty), rep4(p.tree), rep4(p.fire), cntT,
+                                           cntF, cntV);
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            cntT += __shfl_xor(cntT, off);
+            cntF += __shfl_xor(cntF, off);
+            cntV += __shfl_xor(cntV, off);
+        }
+        if (lane == 0) {
+            atomicAdd(&blk_cnt[0], cntV - cntT - cntF);
+            atomicAdd(&blk_cnt[1], cntT);
+            atomicAdd(&blk_cnt[2], cntF);
+        }
+        __syncthreads();  // the new grid (every wave's stores) and the counts are complete
+        grid = Dst;
+    }
+    if (tid != 0) return;
+    steps[e] = n;
+    if (n < 0) {  // finished before this step: graceful no-op (ca_env.py:50-62)
+        reward[e] = 0.0;
+        return;
+    }
+    accu[e] = x - reps;
+    int32_t cE = counts[3 * e + 0], cT = counts[3 * e + 1], cF = counts[3 * e + 2];
+    if (n > 0) {
+        parity[e] = odd ? 0 : 1;
+        cE = blk_cnt[0];
+        cT = blk_cnt[1];
+        cF = blk_cnt[2];
+    }
+    // MoveModify: Move, then Modify at the new position (on the post-CA grid)
+    const int a1 = action[2 * e + 1];
+    int row = pos[2 * e], col = pos[2 * e + 1];
+    move_pos(a0, row, col, H, W, p.up_mask, p.down_mask, p.left_mask, p.right_mask);
+    pos[2 * e] = row;
+    pos[2 * e + 1] = col;
+    uint8_t h = 0;
+    if (a1) {
+        const int v = grid[(int64_t)row * W + col];
+        const int nv = p.effect[v];
+        if (nv >= 0) {
+            grid[(int64_t)row * W + col] = (uint8_t)nv;
+            h = 1;
+            const int c_old = cell_category(v, p.empty, p.tree, p.fire), c_new = cell_category(nv, p.empty, p.tree, p.fire);
+            if (c_old == 0) cE -= 1; else if (c_old == 1) cT -= 1; else if (c_old == 2) cF -= 1;
+            if (c_new == 0) cE += 1; else if (c_new == 1) cT += 1; else if (c_new == 2) cF += 1;
+        }
+    }
+    counts[3 * e + 0] = cE;
+    counts[3 * e + 1] = cT;
+    counts[3 * e + 2] = cF;
+    hit[e] = h;
+    reward[e] = (cT + cF) > 0 ? -((double)cF / (double)(cT + cF)) : (double)NAN;
+    done[e] = cF == 0 ? 1 : 0;
+    rng_step[e] += (uint32_t)n;
+    if (steps_elapsed) steps_elapsed[e] += 1;
 }
 
 template <int NW>
@@ -496,5 +614,40 @@ extern "C" int gca_windy_step(uint8_t* buf0, uint8_t* buf1, const uint8_t* parit
                            pass, dir_mask, E, H, W, empty, tree, fire, counts);
         GCA_CHECK_LAUNCH("windy_exact");
     }
+    return GCA_OK;
+}
+
+extern "C" int gca_bulldozer_step_fused(const gca_bulldozer_params* p, const int32_t* action, double* accu,
+                                        int32_t* steps, uint8_t* done, const double* wind, int64_t wind_stride,
+                                        uint32_t* rng_step, uint8_t* parity, uint8_t* buf0, uint8_t* buf1, int H, int W,
+                                        int32_t* pos, int32_t* counts, uint8_t* hit, double* reward,
+                                        int64_t* steps_elapsed, int E, void* stream) {
+    GCA_CHECK_ARG(p && action && accu && steps && done && wind && rng_step && parity && buf0 && buf1 && pos && counts &&
+                      hit && reward && E > 0 && H > 0,
+                  "bulldozer_step_fused: null argument or empty batch");
+    GCA_CHECK_ARG(W == 256 || W == 512, "bulldozer_step_fused: W must be 256 or 512 (the row-stream CA)");
+    GCA_CHECK_ARG(p->empty == 0 && p->empty < p->tree && p->tree < p->fire && p->fire < 256,
+                  "bulldozer_step_fused: cell codes must be empty = 0 < tree < fire < 256 (the closed-form rule)");
+    GCA_CHECK_ARG(((((uintptr_t)buf0) | ((uintptr_t)buf1)) & 15u) == 0, "bulldozer_step_fused: buffers 16-B aligned");
+    GCA_CHECK_ARG(wind_stride >= 0, "bulldozer_step_fused: wind_stride >= 0");
+    // at most one CA step per env step: accu < 1 on entry, so (t_move + t_shoot) + t_any < 1 for every action
+    double tmax = 0.0;
+    for (int a = 0; a < 9; ++a)
+        for (int b = 0; b < 2; ++b) tmax = fmax(tmax, (p->t_move[a] + p->t_shoot[b]) + p->t_any);
+    GCA_CHECK_ARG(tmax < 1.0, "bulldozer_step_fused: an action can take >= 1 time unit (several CA passes per step): "
+                              "use gca_bulldozer_pre / gca_windy_step / gca_bulldozer_post");
+    const int fsh = W == 256 ? FUSED_SH<1> : FUSED_SH<2>;
+    const int strips = (H + fsh - 1) / fsh;
+    const int threads = 64 * (strips < 16 ? strips : 16);
+    hipStream_t st = (hipStream_t)stream;
+    if (W == 256)
+        hipLaunchKernelGGL(bulldozer_step_fused_kernel<1>, dim3((unsigned)E), dim3(threads), 0, st, *p, action, accu,
+                           steps, done, wind, wind_stride, rng_step, parity, buf0, buf1, H, pos, counts, hit, reward,
+                           steps_elapsed);
+    else
+        hipLaunchKernelGGL(bulldozer_step_fused_kernel<2>, dim3((unsigned)E), dim3(threads), 0, st, *p, action, accu,
+                           steps, done, wind, wind_stride, rng_step, parity, buf0, buf1, H, pos, counts, hit, reward,
+                           steps_elapsed);
+    GCA_CHECK_LAUNCH("bulldozer_step_fused");
     return GCA_OK;
 }

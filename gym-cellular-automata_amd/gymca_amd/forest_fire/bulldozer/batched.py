@@ -9,6 +9,11 @@ wave of the CA kernel:
     gca_bulldozer_interpass  between passes (parity flip + next roll)
     gca_bulldozer_post       Move/Modify (move_modify.py:128-134), reward/done (bulldozer.py:180-216)
 
+or, when every action takes less than one time unit (one CA pass at most per env step) and W is 256 or 512 (the
+bench configs 2 and 5), the same step in ONE launch (gca_bulldozer_step_fused: a workgroup per env; envs without a CA
+step this env step leave after their O(1) work). `fused=None` picks it whenever it applies; the two paths are
+checked to give identical envs (tests/test_gpu_windy.py).
+
 Grids live in two buffers; env e's current grid is buf[parity[e]][e], so envs whose
 RepeatCA yields 0 repeats this step (most of them: ~1 CA step per 13 env steps at
 256^2 with random actions) move no bytes at all. Cell counts are
@@ -27,7 +32,7 @@ from .bulldozer import ACTION_SETS, DEFAULT_WIND, bulldozer_timings, parse_wind
 class BatchedForestFireBulldozerEnv:
     def __init__(self, num_envs, nrows, ncols, device=None, seed=0, env_offset=0, speed_move=0.12, speed_act=0.03,
                  t_move=None, t_shoot=None, t_any=0.001, p_tree=0.90, p_empty=0.10, wind=DEFAULT_WIND,
-                 materialize_obs=True):
+                 materialize_obs=True, fused=None):
         import torch
 
         self.device = dev.require_device(device)
@@ -50,6 +55,10 @@ class BatchedForestFireBulldozerEnv:
         self.params = p
         max_t = max(p.t_move[a] for a in range(9)) + max(p.t_shoot[0], p.t_shoot[1]) + t_any
         self.max_passes = int(math.floor(1.0 + max_t))  # accu < 1 before the step
+        fusable = self.max_passes == 1 and W in (256, 512) and self._empty == 0
+        if fused and not fusable:
+            raise ValueError("fused=True needs W in (256, 512) and at most one CA pass per env step")
+        self.fused = fusable if fused is None else bool(fused)
         kw = dict(device=self.device)
         self.buf = torch.zeros((2, E, H, W), dtype=torch.uint8, **kw)
         self.parity = torch.zeros(E, dtype=torch.uint8, **kw)
@@ -65,6 +74,7 @@ class BatchedForestFireBulldozerEnv:
         w = parse_wind(wind) if isinstance(wind, dict) else np.asarray(wind, dtype=np.float64)
         self.wind = dev.to_device(np.broadcast_to(w.reshape(-1, 9), (E, 9)), torch.float64, self.device)
         self.steps_elapsed = torch.zeros(E, dtype=torch.int64, **kw)
+        self._truncated = torch.zeros(E, dtype=torch.bool, **kw)
 
     # ------------------------------------------------------------------ state
     def grids(self):
@@ -129,6 +139,14 @@ class BatchedForestFireBulldozerEnv:
         a = a.to(torch.int32).reshape(E, 2).contiguous()
         st = dev.stream_ptr(self.device)
         p = self.params
+        if self.fused:
+            call("gca_bulldozer_step_fused", p, dev.ptr(a), dev.ptr(self.accu), dev.ptr(self.steps),
+                 dev.ptr(self.done), dev.ptr(self.wind), 9, dev.ptr(self.rng_step), dev.ptr(self.parity),
+                 dev.ptr(self.buf[0]), dev.ptr(self.buf[1]), H, W, dev.ptr(self.pos), dev.ptr(self.counts),
+                 dev.ptr(self.hit), dev.ptr(self.reward), dev.ptr(self.steps_elapsed), E, st)
+            # done is 0 / 1 bytes: a bool view, no kernel; truncated is a persistent all-False tensor
+            return self._obs(), self.reward, self.done.view(torch.bool), self._truncated, {"hit": self.hit,
+                                                                                           "ca_steps": self.steps}
         call("gca_bulldozer_pre", p, dev.ptr(a), dev.ptr(self.accu), dev.ptr(self.steps), dev.ptr(self.done),
              dev.ptr(self.wind), 9, dev.ptr(self.rng_step), dev.ptr(self.dir_mask), dev.ptr(self.counts), E, st)
         P = self.max_passes
@@ -144,9 +162,8 @@ class BatchedForestFireBulldozerEnv:
              dev.ptr(self.buf[0]), dev.ptr(self.buf[1]), H, W, dev.ptr(self.pos), dev.ptr(self.counts),
              dev.ptr(self.rng_step), dev.ptr(self.done), dev.ptr(self.hit), dev.ptr(self.reward), E, st)
         self.steps_elapsed += (self.steps >= 0).to(torch.int64)
-        terminated = self.done.bool()
-        truncated = torch.zeros_like(terminated)
-        return self._obs(), self.reward, terminated, truncated, {"hit": self.hit, "ca_steps": self.steps}
+        return self._obs(), self.reward, self.done.view(torch.bool), self._truncated, {"hit": self.hit,
+                                                                                       "ca_steps": self.steps}
 
     def ca_step_all(self, dir_mask=None):
         """One forced WindyForestFire step of every env (bench 'CA-only' mode, steps[E] = 1)."""

@@ -115,6 +115,18 @@ int gca_bulldozer_post(const gca_bulldozer_params* p, int last_pass, const int32
                        int32_t* counts, uint32_t* rng_step, uint8_t* done, uint8_t* hit, double* reward,
                        int E, void* stream);
 
+/* The whole ForestFireBulldozer env step in one launch (bulldozer.py:393-400 MDP.update + ca_env.py:27-62 reward /
+ * done), one workgroup per env: the gca_bulldozer_pre bookkeeping, when a CA step is due (steps[e] = 1) the Windy
+ * direction mask and the row-stream CA of gca_windy_step on the env's grid, then gca_bulldozer_post's Move / Modify,
+ * counts, reward, done, hit, rng_step and parity; steps_elapsed (nullable) += 1 for live envs. Identical results to
+ * the three-kernel sequence. Requires W = 256 or 512, empty = 0 < tree < fire, 16-B aligned buffers and one CA pass
+ * at most per env step ((t_move + t_shoot) + t_any < 1 for every action; otherwise GCA_ERR_ARG).            */
+int gca_bulldozer_step_fused(const gca_bulldozer_params* p, const int32_t* action, double* accu, int32_t* steps,
+                             uint8_t* done, const double* wind, int64_t wind_stride, uint32_t* rng_step,
+                             uint8_t* parity, uint8_t* buf0, uint8_t* buf1, int H, int W, int32_t* pos,
+                             int32_t* counts, uint8_t* hit, double* reward, int64_t* steps_elapsed, int E,
+                             void* stream);
+
 /* Move then Modify for E envs (move_modify.py:37-134): action[e] = (move, shoot);
  * uses p->up/down/left/right_mask and p->effect; grid may be NULL (Move only); hit nullable. */
 int gca_move_modify(const gca_bulldozer_params* p, const int32_t* action, int32_t* pos, uint8_t* grid, int H, int W,

@@ -298,3 +298,60 @@ def test_sharded_windy_env_equals_unsharded(device, N):
             assert torch.equal(torch.cat([getattr(shards[0], name), getattr(shards[1], name)]), getattr(full, name))
         assert torch.equal(torch.nan_to_num(torch.cat([shards[0].reward, shards[1].reward])),
                            torch.nan_to_num(full.reward))
+
+
+@pytest.mark.parametrize("N,E,steps", [(256, 48, 120), (512, 16, 120)])
+def test_fused_env_step_equals_three_kernel_step(device, N, E, steps):
+    """gca_bulldozer_step_fused (one launch per env step, a workgroup per env) leaves every env exactly as the
+    gca_bulldozer_pre / gca_windy_step / gca_bulldozer_post sequence does: grids, parity, accu, steps, counts, pos,
+    hit, reward, done, rng_step and steps_elapsed after every step, including envs that finish (no FIRE left) and
+    are stepped again (graceful no-op), and under a hipGraph replay."""
+    import torch
+
+    from gymca_amd import _device as dev
+    from gymca_amd._lib import call
+    from gymca_amd.forest_fire.bulldozer import BatchedForestFireBulldozerEnv
+    from gymca_amd.graph import StepGraph
+
+    envs = [BatchedForestFireBulldozerEnv(E, N, N, device=device, seed=29, fused=f, materialize_obs=False,
+                                          p_tree=0.55, p_empty=0.45) for f in (True, False)]
+    assert envs[0].fused and not envs[1].fused
+    acts = [torch.zeros((E, 2), dtype=torch.int32, device=device) for _ in envs]
+    for env in envs:
+        env.reset(seed=4)
+        # a few envs start without FIRE: done after their first step, then stepped as finished envs
+        g = env.grids()
+        g[: E // 8][g[: E // 8] == 25] = 3
+        env.buf[0].copy_(g)
+        call("gca_count_cells", dev.ptr(env.buf[0]), E, N, N, 0, 3, 25, dev.ptr(env.counts), dev.stream_ptr(device))
+
+    names = ("parity", "accu", "steps", "counts", "pos", "hit", "reward", "done", "rng_step", "steps_elapsed")
+
+    def check(s):
+        a, b = envs
+        assert torch.equal(a.grids(), b.grids()), f"grids, step {s}"
+        for name in names:
+            ta, tb = getattr(a, name), getattr(b, name)
+            assert torch.equal(torch.nan_to_num(ta), torch.nan_to_num(tb)), f"{name}, step {s}"
+
+    def stepper(k):
+        def f():
+            call("gca_random_actions", dev.ptr(acts[k]), E, 0, 13, dev.ptr(envs[k].rng_step), dev.stream_ptr(device))
+            envs[k].step(acts[k])
+        return f
+
+    ca_steps = 0
+    for s in range(steps):
+        for k in range(2):
+            stepper(k)()
+        ca_steps += int((envs[0].steps > 0).sum().item())
+        check(s)
+    assert ca_steps > steps * E // 60  # the CA really ran (~1 env step in 13 at 256^2, 25 at 512^2, live envs)
+    assert int(envs[0].done[: E // 8].sum().item()) == E // 8
+    graph = StepGraph(stepper(0), n_steps=8, device=device, warmup=0)
+    for _ in range(3):
+        graph.replay()
+        for _ in range(8):
+            stepper(1)()
+    torch.cuda.synchronize(device)
+    check("graph")
