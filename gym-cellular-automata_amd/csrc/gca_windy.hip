@@ -428,41 +428,54 @@ __global__ __launch_bounds__(256) void windy_rows_kernel(uint8_t* __restrict__ b
 }
 
 // ------------------------------------------------------------------ the whole ForestFireBulldozer env step, fused
-template <int NW> constexpr int FUSED_SH = NW == 1 ? 16 : 32;  // strip height per wave of the fused step
-// One workgroup per env runs bulldozer.py's MDP.update (:393-400) for that env in one launch: RepeatCA's time
-// bookkeeping (repeat_ca.py:32-45), when a CA step is due the Windy direction mask (ca_windy.py:53-77) and the CA over
-// the env's grid (one wave per 16-row strip, windy_rows_strip: the same bytes as gca_windy_step), then Move / Modify
-// (move_modify.py:128-134) on the new grid and reward / done (bulldozer.py:180-216) from the fused counts. The
-// arithmetic is that of gca_bulldozer_pre / gca_windy_step / gca_bulldozer_post (one CA pass per env step at most,
-// host-checked), so the two paths give identical envs; the multi-kernel path launches four kernels per env step over
-// every env although only ~1 env in 13 takes a CA step, this one launch, and envs without a CA step
-// leave after their O(1) work.
+// strips of the fused step: 32 rows with 16 in flight at W = 256 (8 waves per env: four workgroups per CU, so the
+// launch's 1024 workgroups are resident at once), 16 rows with 8 in flight (the rows kernel's) at W = 512 (16 waves)
+template <int NW> constexpr int FUSED_SH = NW == 1 ? 32 : 16;
+template <int NW> constexpr int FUSED_RD = NW == 1 ? 16 : 8;
+
+// The launch is latency-bound (the stepping envs are few), so the per-env inputs are all loaded up front, before any
+// branch or barrier: one round trip to memory instead of a chain of dependent ones (the env's action, then its
+// accu, then the wind, after the CA the position, the counts ... measured 13.6 us per 1024 x 256^2 env step with
+// the loads where they are used, r03u). A launch of fewer, resident workgroups looping over the envs measured
+// slower still (16.3 us, r03v: each workgroup then pays its envs' chains one after the other).
 template <int NW>
-__global__ __launch_bounds__(1024) void bulldozer_step_fused_kernel(
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) void bulldozer_step_fused_kernel(
     gca_bulldozer_params p, const int32_t* __restrict__ action, double* __restrict__ accu, int32_t* __restrict__ steps,
     uint8_t* __restrict__ done, const double* __restrict__ wind, int64_t wind_stride, uint32_t* __restrict__ rng_step,
     uint8_t* __restrict__ parity, uint8_t* __restrict__ buf0, uint8_t* __restrict__ buf1, int H,
     int32_t* __restrict__ pos, int32_t* __restrict__ counts, uint8_t* __restrict__ hit, double* __restrict__ reward,
     int64_t* __restrict__ steps_elapsed) {
     constexpr int W = 256 * NW;
-    constexpr int FSH = FUSED_SH<NW>;
     __shared__ int32_t blk_cnt[3];
     __shared__ uint32_t blk_mask;
     const int e = blockIdx.x;
     const int tid = threadIdx.x;
-    // ---- RepeatCA bookkeeping (every thread computes n from the same loads; thread 0 writes after the CA)
+    // ---- every per-env input (wave-uniform addresses: scalar loads), issued together
     const bool was_done = done[e] != 0;
-    const int a0 = clampi_dev(action[2 * e], 0, 8), a1s = clampi_dev(action[2 * e + 1], 0, 1);
-    const double x = accu[e] + ((p.t_move[a0] + p.t_shoot[a1s]) + p.t_any);
+    const int32_t act0 = action[2 * e], act1 = action[2 * e + 1];
+    const double acc = accu[e];
+    const bool odd = parity[e] != 0;
+    const int32_t prow = pos[2 * e], pcol = pos[2 * e + 1];
+    const int32_t c0 = counts[3 * e + 0], c1 = counts[3 * e + 1], c2 = counts[3 * e + 2];
+    const uint32_t rs = rng_step[e];
+    const int64_t se = steps_elapsed ? steps_elapsed[e] : 0;
+    double wl[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) wl[k] = wind[(int64_t)e * wind_stride + k];
+    // ---- RepeatCA bookkeeping (repeat_ca.py:32-45, as gca_bulldozer_pre) and the Move (move_modify.py:37-67, as
+    //      gca_bulldozer_post), which does not depend on the CA
+    const int a0 = clampi_dev(act0, 0, 8), a1s = clampi_dev(act1, 0, 1);
+    const double x = acc + ((p.t_move[a0] + p.t_shoot[a1s]) + p.t_any);
     const double reps = trunc(x);  // math.modf
     const int n = was_done ? -1 : (int)reps;
-    const bool odd = parity[e] != 0;
+    int row = prow, col = pcol;
+    move_pos(a0, row, col, H, W, p.up_mask, p.down_mask, p.left_mask, p.right_mask);
     const int64_t HW = (int64_t)H * W;
     uint8_t* grid = (odd ? buf1 : buf0) + e * HW;  // the env's grid after this step
     if (n > 0) {
         if (tid == 0) {
-            blk_mask = windy_mask(wind + (int64_t)e * wind_stride, nullptr, (uint32_t)p.seed, (uint32_t)(p.seed >> 32),
-                                  (uint32_t)(p.env_offset + e), rng_step[e]);
+            blk_mask = windy_mask(wl, nullptr, (uint32_t)p.seed, (uint32_t)(p.seed >> 32), (uint32_t)(p.env_offset + e),
+                                  rs);
             blk_cnt[0] = blk_cnt[1] = blk_cnt[2] = 0;
         }
         __syncthreads();
@@ -472,12 +485,9 @@ __global__ __launch_bounds__(1024) void bulldozer_step_fused_kernel(
         uint8_t* __restrict__ Dst = (odd ? buf0 : buf1) + e * HW;
         const uint32_t lofs = 4 * NW * (uint32_t)lane;
         int32_t cntT = 0, cntF = 0, cntV = 0;
-        // strips of FSH rows with the whole strip's rows in flight at once: only the ~1 env in 13 (256^2; 1 in 25 at
-        // 512^2) with a CA step this env step runs here, so the launch is latency-bound, not occupancy-bound, and a
-        // wave's strip costs one round trip to memory (16 waves cover a 512-row grid in one strip each)
-        for (int s0 = wave * FSH; s0 < H; s0 += nw * FSH)
-            windy_rows_strip<NW, FSH, FSH>(S, Dst, s0, H, m, lofs, rep4(p.empty), rep4(p.tree), rep4(p.fire), cntT,
-                                           cntF, cntV);
+        for (int s0 = wave * FUSED_SH<NW>; s0 < H; s0 += nw * FUSED_SH<NW>)
+            windy_rows_strip<NW, FUSED_SH<NW>, FUSED_RD<NW>>(S, Dst, s0, H, m, lofs, rep4(p.empty), rep4(p.tree),
+                                                            rep4(p.fire), cntT, cntF, cntV);
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) {
             cntT += __shfl_xor(cntT, off);
@@ -499,21 +509,18 @@ __global__ __launch_bounds__(1024) void bulldozer_step_fused_kernel(
         return;
     }
     accu[e] = x - reps;
-    int32_t cE = counts[3 * e + 0], cT = counts[3 * e + 1], cF = counts[3 * e + 2];
+    int32_t cE = c0, cT = c1, cF = c2;
     if (n > 0) {
         parity[e] = odd ? 0 : 1;
         cE = blk_cnt[0];
         cT = blk_cnt[1];
         cF = blk_cnt[2];
     }
-    // MoveModify: Move, then Modify at the new position (on the post-CA grid)
-    const int a1 = action[2 * e + 1];
-    int row = pos[2 * e], col = pos[2 * e + 1];
-    move_pos(a0, row, col, H, W, p.up_mask, p.down_mask, p.left_mask, p.right_mask);
+    // MoveModify (move_modify.py:128-134): Modify at the new position, on the post-CA grid
     pos[2 * e] = row;
     pos[2 * e + 1] = col;
     uint8_t h = 0;
-    if (a1) {
+    if (act1) {
         const int v = grid[(int64_t)row * W + col];
         const int nv = p.effect[v];
         if (nv >= 0) {
@@ -530,8 +537,8 @@ __global__ __launch_bounds__(1024) void bulldozer_step_fused_kernel(
     hit[e] = h;
     reward[e] = (cT + cF) > 0 ? -((double)cF / (double)(cT + cF)) : (double)NAN;
     done[e] = cF == 0 ? 1 : 0;
-    rng_step[e] += (uint32_t)n;
-    if (steps_elapsed) steps_elapsed[e] += 1;
+    rng_step[e] = rs + (uint32_t)n;
+    if (steps_elapsed) steps_elapsed[e] = se + 1;
 }
 
 template <int NW>
