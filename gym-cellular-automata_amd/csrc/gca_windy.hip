@@ -299,13 +299,22 @@ __device__ __forceinline__ RowRaw<NW> load_rowraw(const uint8_t* __restrict__ S,
     return x;
 }
 
-template <int NW>
+// STD: the bulldozer's codes EMPTY 0, TREE 3 (0b00011), FIRE 25 (0b11001): on these three byte values FIRE is bit 4
+// and TREE is bit 0 without bit 4, so both flags cost 3 VALU (shift, and, one bitop3) instead of two byte compares
+// (~9); the fast rule's contract already restricts the cells to the three codes
+template <int NW, bool STD>
 __device__ __forceinline__ RowCls<NW> classify_row(const RowRaw<NW>& x, bool valid, uint32_t Tp, uint32_t Fp) {
     RowCls<NW> o;
 #pragma unroll
     for (int j = 0; j < NW; ++j) {
-        o.f[j] = valid ? bytes_eq01(x.w[j], Fp) : 0u;
-        o.t[j] = valid ? bytes_eq01(x.w[j], Tp) : 0u;
+        if constexpr (STD) {
+            const uint32_t h = x.w[j] >> 4;
+            o.f[j] = valid ? (h & 0x01010101u) : 0u;
+            o.t[j] = valid ? __builtin_amdgcn_bitop3_b32(x.w[j], h, 0x01010101u, 0x20) : 0u;  // a & ~b & c
+        } else {
+            o.f[j] = valid ? bytes_eq01(x.w[j], Fp) : 0u;
+            o.t[j] = valid ? bytes_eq01(x.w[j], Tp) : 0u;
+        }
     }
     const uint32_t prev = wave_shr1(o.f[NW - 1]), next = wave_shl1(o.f[0]);
 #pragma unroll
@@ -320,7 +329,7 @@ __device__ __forceinline__ RowCls<NW> classify_row(const RowRaw<NW>& x, bool val
 // the strip's new-grid counts are added to (cntT, cntF, cntV = cells written). Shared by windy_rows_kernel (one
 // launch per CA pass) and bulldozer_step_fused_kernel (the whole env step), so both write the same bytes. RD: rows of
 // loads in flight ahead of the row being classified (RD = SH: the whole strip at once), SH: the strip's height.
-template <int NW, int SH, int RD>
+template <int NW, int SH, int RD, bool STD>
 __device__ __forceinline__ void windy_rows_strip(const uint8_t* __restrict__ S, uint8_t* __restrict__ Dst, int s0,
                                                  int H, uint32_t m, uint32_t lofs, uint32_t Ep, uint32_t Tp,
                                                  uint32_t Fp, int32_t& cntT, int32_t& cntF, int32_t& cntV) {
@@ -342,14 +351,14 @@ __device__ __forceinline__ void windy_rows_strip(const uint8_t* __restrict__ S, 
     const RowRaw<NW> r_up = load_rowraw<NW>(S, lofs, s0 - 1, H), r_cur = load_rowraw<NW>(S, lofs, s0, H);
 #pragma unroll
     for (int k = 0; k < RD; ++k) ring[k] = load_rowraw<NW>(S, lofs, s0 + 1 + k, H);
-    RowCls<NW> A = classify_row<NW>(r_up, s0 >= 1, Tp, Fp);
-    RowCls<NW> B = classify_row<NW>(r_cur, true, Tp, Fp);
+    RowCls<NW> A = classify_row<NW, STD>(r_up, s0 >= 1, Tp, Fp);
+    RowCls<NW> B = classify_row<NW, STD>(r_cur, true, Tp, Fp);
 
 #pragma unroll
     for (int t = 0; t < SH; ++t) {
         const int Rc = s0 + t;
         // row Rc + 1: loaded RD rows ago; its slot is refilled with row Rc + 1 + RD right away
-        const RowCls<NW> C = classify_row<NW>(ring[t % RD], Rc + 1 < H, Tp, Fp);
+        const RowCls<NW> C = classify_row<NW, STD>(ring[t % RD], Rc + 1 < H, Tp, Fp);
         if (t + RD < SH) ring[t % RD] = load_rowraw<NW>(S, lofs, Rc + 1 + RD, H);
         uint32_t outw[NW];
         int32_t rowT = 0, rowF = 0;
@@ -388,7 +397,7 @@ __device__ __forceinline__ void windy_rows_strip(const uint8_t* __restrict__ S, 
     }
 }
 
-template <int NW>
+template <int NW, bool STD>
 __global__ __launch_bounds__(256) void windy_rows_kernel(uint8_t* __restrict__ buf0, uint8_t* __restrict__ buf1,
                                                          const uint8_t* __restrict__ parity,
                                                          const int32_t* __restrict__ steps, int pass,
@@ -411,7 +420,7 @@ __global__ __launch_bounds__(256) void windy_rows_kernel(uint8_t* __restrict__ b
     // the env's direction mask, forced into an SGPR (a VGPR copy made hipcc rebuild some masks per row)
     const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane((int)dir_mask[env]);
     int32_t cntT = 0, cntF = 0, cntV = 0;
-    windy_rows_strip<NW, GCA_WINDY_RSH, GCA_WINDY_RD>(S, Dst, s0, H, m, lofs, Ep, Tp, Fp, cntT, cntF, cntV);
+    windy_rows_strip<NW, GCA_WINDY_RSH, GCA_WINDY_RD, STD>(S, Dst, s0, H, m, lofs, Ep, Tp, Fp, cntT, cntF, cntV);
     if (counts) {
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) {
@@ -438,7 +447,7 @@ template <int NW> constexpr int FUSED_RD = NW == 1 ? 16 : 8;
 // accu, then the wind, after the CA the position, the counts ... measured 13.6 us per 1024 x 256^2 env step with
 // the loads where they are used, r03u). A launch of fewer, resident workgroups looping over the envs measured
 // slower still (16.3 us, r03v: each workgroup then pays its envs' chains one after the other).
-template <int NW>
+template <int NW, bool STD>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) void bulldozer_step_fused_kernel(
     gca_bulldozer_params p, const int32_t* __restrict__ action, double* __restrict__ accu, int32_t* __restrict__ steps,
     uint8_t* __restrict__ done, const double* __restrict__ wind, int64_t wind_stride, uint32_t* __restrict__ rng_step,
@@ -486,8 +495,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
         const uint32_t lofs = 4 * NW * (uint32_t)lane;
         int32_t cntT = 0, cntF = 0, cntV = 0;
         for (int s0 = wave * FUSED_SH<NW>; s0 < H; s0 += nw * FUSED_SH<NW>)
-            windy_rows_strip<NW, FUSED_SH<NW>, FUSED_RD<NW>>(S, Dst, s0, H, m, lofs, rep4(p.empty), rep4(p.tree),
-                                                            rep4(p.fire), cntT, cntF, cntV);
+            windy_rows_strip<NW, FUSED_SH<NW>, FUSED_RD<NW>, STD>(S, Dst, s0, H, m, lofs, rep4(p.empty),
+                                                                 rep4(p.tree), rep4(p.fire), cntT, cntF, cntV);
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) {
             cntT += __shfl_xor(cntT, off);
@@ -547,8 +556,12 @@ static void launch_rows(uint8_t* b0, uint8_t* b1, const uint8_t* parity, const i
                         hipStream_t st) {
     const int strips = (H + GCA_WINDY_RSH - 1) / GCA_WINDY_RSH;
     const int bpe = (strips + 3) / 4;
-    hipLaunchKernelGGL(windy_rows_kernel<NW>, dim3((unsigned)((int64_t)E * bpe)), dim3(256), 0, st, b0, b1, parity,
-                       steps, pass, dm, H, bpe, rep4(empty), rep4(tree), rep4(fire), counts);
+    if (empty == 0 && tree == 3 && fire == 25)
+        hipLaunchKernelGGL((windy_rows_kernel<NW, true>), dim3((unsigned)((int64_t)E * bpe)), dim3(256), 0, st, b0, b1,
+                           parity, steps, pass, dm, H, bpe, rep4(empty), rep4(tree), rep4(fire), counts);
+    else
+        hipLaunchKernelGGL((windy_rows_kernel<NW, false>), dim3((unsigned)((int64_t)E * bpe)), dim3(256), 0, st, b0, b1,
+                           parity, steps, pass, dm, H, bpe, rep4(empty), rep4(tree), rep4(fire), counts);
 }
 
 // ------------------------------------------------------------------ host API
@@ -647,14 +660,17 @@ extern "C" int gca_bulldozer_step_fused(const gca_bulldozer_params* p, const int
     const int strips = (H + fsh - 1) / fsh;
     const int threads = 64 * (strips < 16 ? strips : 16);
     hipStream_t st = (hipStream_t)stream;
-    if (W == 256)
-        hipLaunchKernelGGL(bulldozer_step_fused_kernel<1>, dim3((unsigned)E), dim3(threads), 0, st, *p, action, accu,
-                           steps, done, wind, wind_stride, rng_step, parity, buf0, buf1, H, pos, counts, hit, reward,
-                           steps_elapsed);
-    else
-        hipLaunchKernelGGL(bulldozer_step_fused_kernel<2>, dim3((unsigned)E), dim3(threads), 0, st, *p, action, accu,
-                           steps, done, wind, wind_stride, rng_step, parity, buf0, buf1, H, pos, counts, hit, reward,
-                           steps_elapsed);
+    const bool std_codes = p->empty == 0 && p->tree == 3 && p->fire == 25;
+#define GCA_FUSED_LAUNCH(NWV, STDV)                                                                                 \
+    hipLaunchKernelGGL((bulldozer_step_fused_kernel<NWV, STDV>), dim3((unsigned)E), dim3(threads), 0, st, *p, action, \
+                       accu, steps, done, wind, wind_stride, rng_step, parity, buf0, buf1, H, pos, counts, hit, reward,   \
+                       steps_elapsed)
+    if (W == 256) {
+        if (std_codes) GCA_FUSED_LAUNCH(1, true); else GCA_FUSED_LAUNCH(1, false);
+    } else {
+        if (std_codes) GCA_FUSED_LAUNCH(2, true); else GCA_FUSED_LAUNCH(2, false);
+    }
+#undef GCA_FUSED_LAUNCH
     GCA_CHECK_LAUNCH("bulldozer_step_fused");
     return GCA_OK;
 }
