@@ -204,40 +204,59 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
         }
     };
 
-    // ---- tile activity map (see gca_alex_step_packed): no FIRE in this tile or the tiles above / below at the
-    //      step's input -> nothing in the tile can change; copy it (act_in only with p_tree == 0, host-checked)
-    if (act_out) {
-        if (act_in) {
-            const uint8_t* A = act_in + (size_t)e * strips;
-            const int anyf = A[s] | (s > 0 ? A[s - 1] : 0) | (s + 1 < strips ? A[s + 1] : 0);
-            if (!anyf) {
-                int cE = 0, cT = 0;
-#pragma unroll 4
-                for (int i = 0; i < SH; ++i) {
-                    const int r = s0 + i;
-                    const uint32_t o = (uint32_t)r * MW + lc;
-                    const uint32_t g = *reinterpret_cast<const uint32_t*>(gE + o);
-                    *reinterpret_cast<uint32_t*>(gO + o) = g;
-                    if (age_in != age_out) *reinterpret_cast<uint2*>(aO + o) = *reinterpret_cast<const uint2*>(aE + o);
-                    cE += __builtin_popcount(bytes_eq01(g, Ep));
-                    cT += __builtin_popcount(bytes_eq01(g, Tp));
-                    if (OBS) write_rgb_row(r, gca_eq_nib(g, Tp), 0u, dflags(draw_bits(r)));
-                }
-                if (lane == 0) act_out[(size_t)e * strips + s] = 0;
-                if (counts) {
+    // ---- quiet tiles: no FIRE in this tile's rows or the row on either side at the step's input -> with p_tree = 0
+    //      nothing in the tile can change (a TREE burns only next to a FIRE; pinecones are a separate pass); copy it.
+    //      Known from the tile activity map when the caller keeps one (gca_alex_step_packed; act_in only with
+    //      p_tree == 0, host-checked), otherwise from the rows themselves: two rows first (in a dense state they
+    //      already hold a FIRE, so the check costs a few VALU), then the other 16 at once
+    //      (r03ac: the episode's first steps, where most tiles are quiet, no longer run the full step on them)
+    // the fire ring's first rows (s0 - R - 1 .. s0 + R - 1) are loaded before the check, which reads two of them: a
+    // dense tile pays no extra round trip
+    uint32_t g_init[NF - 1];
 #pragma unroll
-                    for (int off = 32; off > 0; off >>= 1) {
-                        cE += __shfl_xor(cE, off);
-                        cT += __shfl_xor(cT, off);
-                    }
-                    if (lane == 0) {
-                        if (cE) atomicAdd(counts + 3 * e + 0, cE);
-                        if (cT) atomicAdd(counts + 3 * e + 1, cT);
-                    }
-                }
-                return;
+    for (int t = 0; t < NF - 1; ++t) g_init[t] = graw(s0 - R - 1 + t);
+    bool quiet = false;
+    if (act_out && act_in) {
+        const uint8_t* A = act_in + (size_t)e * strips;
+        quiet = !(A[s] | (s > 0 ? A[s - 1] : 0) | (s + 1 < strips ? A[s + 1] : 0));
+    } else if constexpr (!GROW) {
+        auto has_fire = [&](uint32_t x) {  // some byte of x is the FIRE code (exact: the zero-byte test of x ^ Fp)
+            const uint32_t v = x ^ Fp;
+            return (v - 0x01010101u) & ~v & 0x80808080u;
+        };
+        if (__ballot((has_fire(g_init[R]) | has_fire(g_init[R + 1])) != 0u) == 0ull) {  // rows s0 - 1, s0
+            uint32_t f = 0u;
+#pragma unroll
+            for (int i = 1; i <= SH; ++i) f |= has_fire(graw(s0 + i));
+            quiet = __ballot(f != 0u) == 0ull;
+        }
+    }
+    if (quiet) {
+        int cE = 0, cT = 0;
+#pragma unroll 4
+        for (int i = 0; i < SH; ++i) {
+            const int r = s0 + i;
+            const uint32_t o = (uint32_t)r * MW + lc;
+            const uint32_t g = *reinterpret_cast<const uint32_t*>(gE + o);
+            *reinterpret_cast<uint32_t*>(gO + o) = g;
+            if (age_in != age_out) *reinterpret_cast<uint2*>(aO + o) = *reinterpret_cast<const uint2*>(aE + o);
+            cE += __builtin_popcount(bytes_eq01(g, Ep));
+            cT += __builtin_popcount(bytes_eq01(g, Tp));
+            if (OBS) write_rgb_row(r, gca_eq_nib(g, Tp), 0u, dflags(draw_bits(r)));
+        }
+        if (act_out && lane == 0) act_out[(size_t)e * strips + s] = 0;
+        if (counts) {
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) {
+                cE += __shfl_xor(cE, off);
+                cT += __shfl_xor(cT, off);
+            }
+            if (lane == 0) {
+                if (cE) atomicAdd(counts + 3 * e + 0, cE);
+                if (cT) atomicAdd(counts + 3 * e + 1, cT);
             }
         }
+        return;
     }
 
     // ---- fire ring in LDS: the FIRE flags (0x01 bytes) of rows r-R-1 .. r+R, one dword per lane and row, each row
@@ -253,7 +272,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
         FR[(sl + NF) * 64 + lane] = v;
     };
 #pragma unroll
-    for (int t = 0; t < NF - 1; ++t) ring_put(t, bytes_eq01(graw(s0 - R - 1 + t), Fp));
+    for (int t = 0; t < NF - 1; ++t) ring_put(t, bytes_eq01(g_init[t], Fp));
     uint32_t dring[6];
 #pragma unroll
     for (int t = 0; t < 5; ++t) dring[t] = dflags(draw_bits(s0 - 3 + t));

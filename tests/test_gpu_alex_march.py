@@ -190,3 +190,29 @@ def test_march_other_cell_codes(device):
     assert np.array_equal(g1, g0), np.argwhere(g1 != g0)[:5]
     assert np.array_equal(a1, a0) and np.array_equal(c1, c0) and np.array_equal(t1, t0)
     assert (g1[:, 5, 10:20] == 9).all()
+
+
+def test_march_quiet_tiles_from_the_grid(device):
+    """Without an activity map (act_in = NULL) at p_tree = 0 the step copies tiles with no FIRE in their rows or the
+    row on either side, found from the grid itself: fires placed on tile-boundary rows (the last row of a tile, the
+    first row of the next, the grid's first and last rows) and a fire-free env; grid, ages (not in place), counts and
+    the activity map equal the tiled kernel's over four steps."""
+    E, H, W = 3, 96, 256
+    case = make_case(E, H, W, 61, p_tree=0.0, dousing_p=0.2, fire_p=0.0)
+    case["grid"][0, 15, 100] = 2    # last row of tile 0: tiles 0 and 1 are not quiet
+    case["grid"][0, 48, 3:250:31] = 2  # first row of tile 3: tiles 2 and 3
+    case["grid"][2, 0, 0] = 2       # the grid's first row
+    case["grid"][2, 95, 255] = 2    # the grid's last row
+    case["age"][case["grid"] == 2] = 4
+    p = params(H, 0.0, seed=13)
+    es, _ = slopes(device, altitude(E, H, W, 61))
+    coal = _coalesced(device, es)
+    vd, bits = _layers(device, case)
+    for s in range(4):
+        rs = np.full(E, 11 * s + 1, np.uint32)
+        g0, a0, c0, t0, _ = _run(device, "gca_alex_step_packed", p, case, coal, rs, vd, bits)
+        g1, a1, c1, t1, _ = _run(device, "gca_alex_step_march", p, case, es, rs, vd, bits)
+        assert np.array_equal(g1, g0), f"step {s}: {np.argwhere(g1 != g0)[:5]}"
+        assert np.array_equal(a1, a0) and np.array_equal(c1, c0) and np.array_equal(t1, t0), f"step {s}"
+        case["grid"], case["age"] = g1, a1
+    assert (case["grid"][1] != 2).all()
