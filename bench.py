@@ -344,7 +344,8 @@ def bench_alex(args, world, rank, device, pg):
     # grid/age/dousing traffic. Reported separately; the headline above is the dense mid-episode state.
     dt_sp, kern_sp = timed_loop(step, args.steps, args.warmup, pg, device, reps=3, prepare=env.reset)
     res["episode_start"] = {"cell_updates_per_s": world * E * N * N * args.steps / dt_sp,
-                            "kernel_ms": kern_sp * 1e3, "state": "reset state (2 fires per env), fire-sparsity skip"}
+                            "kernel_ms": kern_sp * 1e3, "state": "reset state (2 fires per env): tiles with no FIRE nearby copied (found from the grid), "
+                                     "fire-sparsity skip elsewhere"}
     # the same episode start with the opt-in tile activity map (tiles without fire nearby copied, not stepped)
     env.set_tile_skip(True)
     dt_ts, kern_ts = timed_loop(step, args.steps, args.warmup, pg, device, reps=3, prepare=env.reset)
