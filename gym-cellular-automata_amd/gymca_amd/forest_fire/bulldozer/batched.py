@@ -131,7 +131,9 @@ class BatchedForestFireBulldozerEnv:
 
     # ------------------------------------------------------------------ step
     def step(self, action):
-        """action: (E, 2) int (move in [0,9), shoot in {0,1}); device tensor or numpy."""
+        """action: (E, 2) int (move in [0,9), shoot in {0,1}); device tensor or numpy. Returns (obs, reward,
+        terminated, truncated, info) as device tensors that the next step overwrites in place (terminated is a bool
+        view of `done`, truncated a persistent all-False tensor: no kernel launch per step); clone to keep them."""
         import torch
 
         E, H, W = self.num_envs, self.nrows, self.ncols
