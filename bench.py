@@ -261,6 +261,7 @@ def bench_alex(args, world, rank, device, pg):
         "timing": detail,
         "kernel": ("alex_march_kernel" if getattr(env, "march", False) else
                    "alex_step_kernel" + {"packed": "<ES, PK>", "edge": "<ES>", "planes": ""}[args.slope_layout]),
+        "kernel_key": headline_kernel_key(env),
     }
     if getattr(env, "march", False) and rank == 0:
         res["tiled_kernel_ms"] = tiled_kernel_ms(env, device)
@@ -344,14 +345,9 @@ def bench_alex(args, world, rank, device, pg):
     # grid/age/dousing traffic. Reported separately; the headline above is the dense mid-episode state.
     dt_sp, kern_sp = timed_loop(step, args.steps, args.warmup, pg, device, reps=3, prepare=env.reset)
     res["episode_start"] = {"cell_updates_per_s": world * E * N * N * args.steps / dt_sp,
-                            "kernel_ms": kern_sp * 1e3, "state": "reset state (2 fires per env): tiles with no FIRE nearby copied (found from the grid), "
-                                     "fire-sparsity skip elsewhere"}
-    # the same episode start with the opt-in tile activity map (tiles without fire nearby copied, not stepped)
-    env.set_tile_skip(True)
-    dt_ts, kern_ts = timed_loop(step, args.steps, args.warmup, pg, device, reps=3, prepare=env.reset)
-    res["episode_start"]["tile_skip"] = {"cell_updates_per_s": world * E * N * N * args.steps / dt_ts,
-                                         "kernel_ms": kern_ts * 1e3}
-    env.set_tile_skip(args.tile_skip)
+                            "kernel_ms": kern_sp * 1e3,
+                            "state": "reset state (2 fires per env): tiles with no FIRE nearby copied (found from the "
+                                     "grid), fire-sparsity skip elsewhere"}
     return res
 
 
@@ -429,12 +425,14 @@ def bench_windy(args, world, rank, device, pg):
         env.step(action)
 
     K = max(args.steps, 40)
-    dt_eager, _ = timed_loop(lambda ev: one_step(), K, args.warmup, pg, device)
-    # the same steps replayed from one HIP graph per G env steps (no host launch overhead)
+    # every loop starts from the same reset state (env.reset: the seeded initial distribution, RNG counters at 0), so
+    # the eager and graph figures time the same stretch of the same trajectories
     G = 8
-    graph = StepGraph(one_step, n_steps=G, device=device)
     Kg = max(K // G, 5)
-    dt_env, _ = timed_loop(lambda ev: graph.replay(), Kg, 2, pg, device)
+    dt_eager, _ = timed_loop(lambda ev: one_step(), Kg * G, args.warmup, pg, device, reps=3, prepare=env.reset)
+    # the same steps replayed from one HIP graph per G env steps (no host launch overhead)
+    graph = StepGraph(one_step, n_steps=G, device=device)
+    dt_env, _ = timed_loop(lambda ev: graph.replay(), Kg, 2, pg, device, reps=3, prepare=env.reset)
     # CA-only (steps[E] = 1 forced), dense variant {0:.1, 3:.6, 25:.3}
     g = env.grids()
     u = torch.rand(g.shape, device=device)
@@ -473,7 +471,8 @@ def bench_windy(args, world, rank, device, pg):
     return {
         "config": "ForestFireBulldozer 256x256, 1024 envs/GPU, WindyForestFire",
         "env_steps_per_s": world * E * Kg * G / dt_env,
-        "env_steps_per_s_eager": world * E * K / dt_eager,
+        "env_steps_per_s_eager": world * E * Kg * G / dt_eager,
+        "loops": f"eager and graph: {Kg * G} env steps from the same reset state, median of 3",
         "env_step_graph": f"hipGraph of {G} env steps (random actions + " + (
             "gca_bulldozer_step_fused: RepeatCA, Windy CA, Move/Modify and reward in one launch)" if env.fused else
             "RepeatCA/Windy passes + Move/Modify + reward)"),
@@ -517,6 +516,9 @@ def bench_windy512(args, world, rank, device, pg):
             stats.gather(env.done, env.reward, env.steps_elapsed, async_op=async_op)
 
     K = max(args.steps, 40)
+    G = 8
+    Kg = max(K // G, 5)
+    K = Kg * G  # every loop: the same K env steps from the same reset state (env.reset), median of 3
 
     def eager(ev):
         one_step()
@@ -526,17 +528,15 @@ def bench_windy512(args, world, rank, device, pg):
         one_step()
         gather(async_op=True)
 
-    dt_eager, _ = timed_loop(eager, K, args.warmup, pg, device)
-    dt_async, _ = timed_loop(overlapped, K, args.warmup, pg, device)
-    G = 8
+    dt_eager, _ = timed_loop(eager, K, args.warmup, pg, device, reps=3, prepare=env.reset)
+    dt_async, _ = timed_loop(overlapped, K, args.warmup, pg, device, reps=3, prepare=env.reset)
     graph = StepGraph(one_step, n_steps=G, device=device)
 
     def seg(ev):
         graph.replay()
         gather()
 
-    Kg = max(K // G, 5)
-    dt_g, _ = timed_loop(seg, Kg, 2, pg, device)
+    dt_g, _ = timed_loop(seg, Kg, 2, pg, device, reps=3, prepare=env.reset)
     # CA-only at HBM scale: one forced Windy step of every env, 268 MB per buffer (beyond the 256 MB
     # Infinity Cache, unlike config 2's 64 MiB pair), dense {0:.1, 3:.6, 25:.3}, beside a same-size copy
     ca = windy_ca_only(env, K, args.warmup, pg, device)
@@ -546,6 +546,7 @@ def bench_windy512(args, world, rank, device, pg):
                          "pre / Windy passes / post kernels"),
             "env_steps_per_s_eager_gather_every_step": world * E * K / dt_eager,
             "env_steps_per_s_async_gather_every_step": world * E * K / dt_async,
+            "loops": f"graph / eager / async: {K} env steps each from the same reset state, median of 3",
             "gather": ("RCCL all_gather_into_tensor of reward f32 | length | done u8 per env into a reused buffer "
                        f"(gymca_amd.distributed.StatsGather: 1 pack + 1 collective), world {world}")
                       if world > 1 else "none (1 GPU)",
@@ -859,34 +860,65 @@ def tiled_kernel_ms(env, device, K=10, reps=3):
     return sorted(times)[len(times) // 2]
 
 
-def _pmc_entry(args):
-    """The committed PMC summary entry (profiles/pmc_traffic.json) of this run's headline kernel, if it is the profiled
-    workload."""
-    if args.envs != 4096 or args.size != 256:
+# the sources a kernel is compiled from (csrc/), hashed into every profiles/pmc_traffic.json entry by
+# scripts/pmc_summary.py: a committed profile describes the timed kernel only while these files are unchanged
+KERNEL_SOURCES = {"alex_march": ("gca_alex_march.hip", "gca_alex_rule.h", "gca_common.h"),
+                  "alex_step": ("gca_alex.hip", "gca_alex_rule.h", "gca_common.h")}
+
+
+def kernel_src_sha(short_name):
+    """sha256 (16 hex digits) of the csrc/ sources of kernel family `short_name` (+ include/gca.h), or None."""
+    import hashlib
+
+    base = short_name.split("<", 1)[0]
+    files = KERNEL_SOURCES.get(base)
+    if files is None:
         return None
+    h = hashlib.sha256()
+    for f in (*(os.path.join(ROOT, "gym-cellular-automata_amd", "csrc", x) for x in files),
+              os.path.join(ROOT, "include", "gca.h")):
+        try:
+            with open(f, "rb") as fh:
+                h.update(fh.read())
+        except OSError:
+            return None
+    return h.hexdigest()[:16]
+
+
+def headline_kernel_key(env):
+    """The rocprof short name (scripts/pmc_summary.py) of the template instance env.ca_step() launches."""
+    R = int(env.alex_params.R)
+    grow = "true" if env.alex_params.p_tree > 0 else "false"
+    if getattr(env, "march", False):
+        return f"alex_march<{R}, false, {grow}>"
+    es = "true" if env.slope_layout in ("packed", "edge") else "false"
+    pk = "true" if env.slope_layout == "packed" else "false"
+    return f"alex_step<{R}, 0, true, {es}, {pk}, false>"
+
+
+def profile_entry(args, key):
+    """The committed PMC summary entry (profiles/pmc_traffic.json) of the timed headline kernel `key`, with its
+    provenance: the entry counts only when it was profiled on this workload from the SAME kernel sources (source hash
+    recorded by scripts/pmc_summary.py); otherwise its figures are not this build's and the bench reports null."""
+    info = {"key": key, "tag": None, "src_sha": kernel_src_sha(key), "profile_src_sha": None, "match": False}
+    if args.envs != 4096 or args.size != 256:
+        info["why"] = "not the profiled workload (4096 x 256^2)"
+        return None, info
     try:
         data = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
     except (ValueError, OSError):
-        return None
-    want = {"packed": "alex_march<6, false>" if args.step_kernel != "tiled" else "alex_step<6, 0, true, true, true>",
-            "edge": "alex_step<6, 0, true, true, false>",
-            "planes": "alex_step<6, 0, true, false, false>"}[args.slope_layout]
-    return data.get(want)
-
-
-def measured_valu_busy(args):
-    """VALU-busy share of the SIMDs over the headline kernel's launch (profiles/pmc_traffic.json: SQ_ACTIVE_INST_VALU in
-    quad-cycles x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs), scripts/pmc_summary.py)."""
-    e = _pmc_entry(args)
-    return None if e is None else e.get("valu_busy")
-
-
-def measured_traffic(args):
-    """HBM bytes per headline launch from the committed rocprofv3 PMC summary (profiles/pmc_traffic.json, written by
-    scripts/pmc_summary.py: 2*FETCH_SIZE + WRITE_SIZE, the gfx950 correction, calibrated for every load width the
-    kernels issue by scripts/fetch_calib.hip) — only when this run is the profiled workload."""
-    e = _pmc_entry(args)
-    return None if e is None else e.get("bytes_per_launch")
+        info["why"] = "no profiles/pmc_traffic.json"
+        return None, info
+    e = data.get(key)
+    if e is None:
+        info["why"] = "the timed kernel has no committed profile"
+        return None, info
+    info.update(tag=e.get("tag"), profile_src_sha=e.get("src_sha"))
+    if e.get("src_sha") is None or e.get("src_sha") != info["src_sha"]:
+        info["why"] = "the committed profile predates the kernel's current sources"
+        return None, info
+    info["match"] = True
+    return e, info
 
 
 def copy_bandwidth(device, nbytes=2 << 30, reps=10):
@@ -945,7 +977,12 @@ def main():
         if dropins is not None:
             dropins["bulldozer_256"]["cpu_baseline"] = cpu_legs["bulldozer_env_256"]
             dropins["helicopter_5x5"]["cpu_baseline"] = cpu_legs["helicopter_5x5"]
-    traffic = measured_traffic(args)
+    # HBM bytes per headline launch (2*FETCH_SIZE + WRITE_SIZE, the gfx950 correction, calibrated by
+    # scripts/fetch_calib.hip) and VALU busy (SQ_ACTIVE_INST_VALU x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)) from the
+    # committed rocprofv3 summary of the SAME kernel (template and sources), else null
+    prof, prof_info = profile_entry(args, alex["kernel_key"])
+    traffic = None if prof is None else prof.get("bytes_per_launch")
+    valu_busy = None if prof is None else prof.get("valu_busy")
     copy_gbs = copy_bandwidth(device)
     if rank == 0:
         out = {
@@ -988,7 +1025,8 @@ def main():
                          "survey_bytes_per_cell": ALEX_BYTES_PER_CELL,
                          "survey_equiv_gbs": alex["survey_equiv_gbs"],
                          "survey_equiv_frac": alex["survey_equiv_gbs"] / HBM_PEAK_GBS,
-                         "valu_busy": measured_valu_busy(args),
+                         "valu_busy": valu_busy,
+                         "profile": prof_info,
                          "slope_layout": args.slope_layout,
                          "moved_bytes_per_cell": ALEX_BYTES[args.slope_layout],
                          "moved_gbs": alex["achieved_gbs"],

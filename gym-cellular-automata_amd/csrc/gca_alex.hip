@@ -28,10 +28,8 @@
 
 namespace {
 
-#ifndef GCA_ALEX_TH
-#define GCA_ALEX_TH 16  // tile rows (A/B hook: 32 rows = 512 threads, run with GCA_ALEX_WGS=2)
-#endif
-constexpr int TH = GCA_ALEX_TH;
+// tile rows (r02n: 32-row tiles of 512 threads, two workgroups per CU, measured 1.82 vs 1.44 ms)
+constexpr int TH = 16;
 constexpr int NT = 16 * TH;  // threads per workgroup (16 lanes per image row)
 constexpr int TW = 256;
 constexpr int CW = TW + 32;  // staged columns: [c0-16, c0+TW+16)
@@ -43,10 +41,7 @@ constexpr int CW = TW + 32;  // staged columns: [c0-16, c0+TW+16)
 // rows (tr, tr+1) of the wave, so the row pitch must be a multiple of 64 dwords for those 16 lanes to stay
 // on 16 distinct q's: CWP = 320 (the unpadded 288 ≡ 32 mod 64 put lanes q and q' = q+-8 of adjacent rows
 // on one bank: 2-way conflicts on every heat-phase read, 7.9e7 conflict cycles per launch in r01o).
-#ifndef GCA_ALEX_CWP
-#define GCA_ALEX_CWP 320
-#endif
-constexpr int CWP = GCA_ALEX_CWP;
+constexpr int CWP = 320;
 static_assert(CWP >= CW, "staged row fits");
 __host__ __device__ constexpr int pcol(int c) { return 16 * (c >> 4) + 4 * ((((c >> 2) & 3) + (c >> 6)) & 3) + (c & 3); }
 static_assert(CWP % 4 == 0, "16-B aligned rows");
@@ -112,34 +107,15 @@ template <class T, class S> __device__ __forceinline__ T bitcast_(S s) {
 // 16j + i; the env's dousing counts are 0/1) and the edge slopes are stored coalesced: inside every 256-column
 // row segment of a plane, column 16q + 4m + j sits at position 64m + 4q + j, so the 16 lanes of an image row
 // read 256 contiguous bytes per load instruction. 23.125 B of HBM traffic per cell instead of 25.
-#ifndef GCA_ALEX_WGS
-#define GCA_ALEX_WGS 4
-#endif
-// GLDS (PK only): after the heat phase the column-prefix LDS is dead, so two of the seven edge-slope loads of the
-// direction pass (L2, L3, then L6) land there by LDS-DMA (global_load_lds_dwordx4, no VGPR destination) beside the
-// two-deep register ring (L0/L4, L1/L5): four loads in flight per wave instead of two. The ring and DMA loads are
-// inline asm, counted by hand (s_waitcnt vmcnt(N) with N = the loads issued after the one waited for); hipcc's own
-// loads are all retired before the first of them (the ties at the end of the heat phase). Bit-exact (the packed-kernel
-// GPU tests), but 2 % SLOWER on the headline (r02h: 1.460 vs 1.433 ms; profiles/r02h), so it stays off: more slope
-// bytes in flight is not what bounds the step.
-#ifndef GCA_ALEX_PRIO
-// Wave priorities (s_setprio) along a tile's phase chain. Default 5: 3 while a tile issues its staging loads, 2 through
-// the LDS writes and the column prefix (the phases in front of the workgroup's last barrier), 0 from the heat phase on,
-// so the SIMD arbiter lets waves that hold up a barrier issue ahead of the barrier-free heat / slope / Philox work of the
-// other workgroups. r02r (profiles/r02r): 1.405 vs 1.434 ms (-2.0 %) on the headline, +4 % on the sparse episode-start
-// state; other levels: 1 = 3 for the staging loads then 0 (-0.6 %); 2 = 1 + 3 for the stores (-0.6 %); 3 = 2 + the
-// direction pass at 2 above the heat phase (+21 %); 4 = 5 with the heat phase at 1 (+1 %); 0 = off.
-#define GCA_ALEX_PRIO 5
-#endif
-#ifndef GCA_ALEX_GLDS
-#define GCA_ALEX_GLDS 0
-#endif
-typedef float f4v __attribute__((ext_vector_type(4)));
-// bytes of the column-prefix region: (RR + 1) rows of CWP dwords; with GLDS at least the 4 waves x 8 KiB of slope slots
-// it hosts after the heat phase (small radii stage fewer rows)
-__host__ __device__ constexpr int cp_bytes(int RR, bool pk) {
-    return (GCA_ALEX_GLDS && pk && 4 * (RR + 1) * CWP < 32768) ? 32768 : 4 * (RR + 1) * CWP;
-}
+constexpr int WGS = 4;  // workgroups per CU (launch bounds)
+// Wave priorities (s_setprio) along a tile's phase chain: 3 while a tile issues its staging loads, 2 through the LDS
+// writes and the column prefix (the phases in front of the workgroup's last barrier), 0 from the heat phase on, so the
+// SIMD arbiter lets waves that hold up a barrier issue ahead of the barrier-free heat / slope / Philox work of the other
+// workgroups. r02r (profiles/r02r): 1.405 vs 1.434 ms (-2.0 %) on the headline, +4 % on the sparse episode-start state;
+// the slope-streaming pass at 2 above the heat phase measured +21 %. (r02h: two of the seven slope loads by LDS-DMA into
+// the dead column prefix, four loads in flight per wave, measured 2 % slower and was removed.)
+// bytes of the column-prefix region: (RR + 1) rows of CWP dwords
+__host__ __device__ constexpr int cp_bytes(int RR, bool) { return 4 * (RR + 1) * CWP; }
 // OBS colour table: after the column prefix, the fire bitmask and the 16-float LUT, 16-B aligned (6 float4)
 __host__ __device__ constexpr int obs_col_off(int RR, bool pk) {
     return (cp_bytes(RR, pk) + 2 * RR * (TW + 32) / 16 + 64 + 15) & ~15;
@@ -156,25 +132,9 @@ struct AlexObs {
     float* rgb;              // [E][H][W][3]
 };
 
-#ifdef GCA_ALEX_STAMPS  // A/B diagnostics build only: s_memtime at the phase boundaries of sampled PK workgroups
-constexpr int STAMP_SAMPLES = 4096, STAMP_N = 7;
-__device__ unsigned long long g_alex_stamps[STAMP_SAMPLES][4][STAMP_N];
-#define ALEX_STAMP(i)                                                                                   \
-    do {                                                                                                \
-        if (PK && stamp_slot >= 0) {                                                                     \
-            unsigned long long t_;                                                                      \
-            __builtin_amdgcn_sched_barrier(0);                                                          \
-            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");               \
-            __builtin_amdgcn_sched_barrier(0);                                                          \
-            if ((threadIdx.x & 63) == 0) g_alex_stamps[stamp_slot][threadIdx.x >> 6][i] = t_;          \
-        }                                                                                               \
-    } while (0)
-#else
-#define ALEX_STAMP(i) do {} while (0)
-#endif
 
 template <int R, int MODE, bool FAST, bool ES, bool PK = false, bool OBS = false>
-__global__ __launch_bounds__(NT, GCA_ALEX_WGS) void alex_step_kernel(
+__global__ __launch_bounds__(NT, WGS) void alex_step_kernel(
     gca_alex_params p, int H, int W, int tiles_r, int tiles_c, const uint8_t* __restrict__ grid_in,
     uint8_t* __restrict__ grid_out, const int16_t* age_in, int16_t* age_out,  // no __restrict__: PK updates in place
     const uint8_t* __restrict__ veg, const uint8_t* __restrict__ den, const uint8_t* __restrict__ dousing,
@@ -207,10 +167,6 @@ __global__ __launch_bounds__(NT, GCA_ALEX_WGS) void alex_step_kernel(
     const int lb = (xcd < rn8 ? xcd * (qn8 + 1) : rn8 * (qn8 + 1) + (xcd - rn8) * qn8) + slot;
     const int e = lb / tiles;
     const int tile = lb - e * tiles;
-#ifdef GCA_ALEX_STAMPS
-    const int stamp_slot = (lb % 64 == 0 && lb / 64 < STAMP_SAMPLES) ? lb / 64 : -1;
-#endif
-    ALEX_STAMP(0);
     const int r0 = (tile / tiles_c) * TH, c0 = (tile % tiles_c) * TW;
     const int64_t HW = (int64_t)H * W;
     const uint8_t* gE = grid_in + (int64_t)e * HW;
@@ -218,7 +174,7 @@ __global__ __launch_bounds__(NT, GCA_ALEX_WGS) void alex_step_kernel(
     const uint16_t* dbE = reinterpret_cast<const uint16_t*>(dousing) + (int64_t)e * (HW >> 4);  // PK: dousing bits
     static_assert(!PK || (ES && FAST && MODE == 0), "packed layout: edge slopes, FAST shape, Philox mode");
     const int tid = threadIdx.x;
-    if (GCA_ALEX_PRIO) __builtin_amdgcn_s_setprio(3);  // (A/B hook) issue this tile's loads ahead of other waves' compute
+    __builtin_amdgcn_s_setprio(3);  // issue this tile's loads ahead of other waves' compute
     const bool rows16 = FAST || (((W & 15) == 0) &&
                                  ((((uintptr_t)grid_in) | ((uintptr_t)dousing) | ((uintptr_t)grid_out) |
                                    ((uintptr_t)veg) | ((uintptr_t)den) | ((uintptr_t)age_in) | ((uintptr_t)age_out) |
@@ -295,15 +251,9 @@ __global__ __launch_bounds__(NT, GCA_ALEX_WGS) void alex_step_kernel(
     constexpr int NPL = ES ? 4 : 8;
     const float* psE = p_slope + (size_t)e * NPL * HW;  // wave-uniform
     auto load_ps = [&](int k, float4 (&v)[4]) {
-#ifdef GCA_ABL_R1ROW  // ablation (wrong results): loads 4..6 re-read load 3's addresses instead of row r+1 (r02h: the
-                      // launch's FETCH then equals the algorithmic reads, 20.13 B/cell vs 24.05, at -1 % time)
-        const int plane = ES ? (k < 4 ? k : 3) : k;
-        const int dr = 0;
-#else
         const int plane = ES ? (k < 4 ? k : 6 - k) : k;
         // ES rows r+1 (k >= 4): row H-1 (a border row: every value killed) reads itself instead
         const int dr = (ES && k >= 4 && r + 1 < H) ? 1 : 0;
-#endif
         const float* src = psE + (uint32_t)(plane * (uint32_t)HW) + lo + (uint32_t)(dr * W);
         if (vec) {
             // PK: coalesced segment order, lane q's columns 16q + 4m .. +3 at segment position 64m + 4q
@@ -320,46 +270,6 @@ __global__ __launch_bounds__(NT, GCA_ALEX_WGS) void alex_step_kernel(
         }
     };
     float4 psbuf[2][4];
-    // ---- GLDS: hand-counted slope loads (see GCA_ALEX_GLDS). Lane byte offset of load k in the env's planes
-    //      (PK segment order: lane q's float4 m at 64m - 12q floats from its cell offset) + offset:256m.
-    constexpr bool GL = PK && (GCA_ALEX_GLDS != 0);
-    f4v ring[2][4];
-    auto ps_off = [&](int k) -> uint32_t {
-        const int plane = k < 4 ? k : 6 - k;
-        const int dr = (k >= 4 && r + 1 < H) ? 1 : 0;
-        return 4u * ((uint32_t)plane * (uint32_t)HW + lo + (uint32_t)(dr * W)) - 48u * (uint32_t)q;
-    };
-    auto gl_ring = [&](int k, f4v (&v)[4]) {
-        const uint32_t o = ps_off(k);
-        asm volatile(
-            "global_load_dwordx4 %0, %4, %5\n\tglobal_load_dwordx4 %1, %4, %5 offset:256\n\t"
-            "global_load_dwordx4 %2, %4, %5 offset:512\n\tglobal_load_dwordx4 %3, %4, %5 offset:768"
-            : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3])
-            : "v"(o), "s"(psE)
-            : "memory");
-    };
-    // LDS slots (byte offsets in smem): wave w owns [8 KiB w, 8 KiB w + 8 KiB) of the dead column prefix; 4 KiB per
-    // load, instruction m's 1 KiB at +1024 m, lane l's 16 B at +16 l (the LDS-DMA's lane-linear image)
-    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint32_t slot_off = 8192u * wv;
-    const uint32_t lds_base = (uint32_t)__builtin_amdgcn_readfirstlane(
-        (uint32_t)(uintptr_t)((__attribute__((address_space(3))) unsigned char*)smem) + slot_off);
-    auto gl_lds = [&](int k, uint32_t slot) {  // slot 0 / 1
-        const uint32_t o = ps_off(k);
-        const uint32_t b = lds_base + 4096u * slot;
-        uint32_t keep;
-        asm volatile(
-            "s_mov_b32 %0, m0\n\t"
-            "s_mov_b32 m0, %5\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %9\n\t"
-            "s_mov_b32 m0, %6\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %9\n\t"
-            "s_mov_b32 m0, %7\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %3, %9\n\t"
-            "s_mov_b32 m0, %8\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %4, %9\n\t"
-            "s_mov_b32 m0, %0"
-            : "=&s"(keep)
-            : "v"(o), "v"(o + 256u), "v"(o + 512u), "v"(o + 768u), "s"(b), "s"(b + 1024u), "s"(b + 2048u),
-              "s"(b + 3072u), "s"(psE)
-            : "memory");
-    };
     uint32_t agew[8];
     auto load_ages = [&]() {
         if (vec) {
@@ -527,7 +437,7 @@ __global__ __launch_bounds__(NT, GCA_ALEX_WGS) void alex_step_kernel(
         }
         if (tid == 0) act_out[(size_t)e * tiles_all + tile] = 0;
     }
-    if (GCA_ALEX_PRIO) __builtin_amdgcn_s_setprio(GCA_ALEX_PRIO >= 4 ? 2 : 0);
+    __builtin_amdgcn_s_setprio(2);
     int near_fire = 0;  // a FIRE cell within one row of the tile (rows r0-1 .. r0+TH) in this thread's chunks
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
@@ -559,7 +469,6 @@ __global__ __launch_bounds__(NT, GCA_ALEX_WGS) void alex_step_kernel(
         wg_need = __syncthreads_or(near_fire) != 0;
     else
         __syncthreads();
-    ALEX_STAMP(1);
     uint32_t treeB = 0u, emptyB = 0u;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -597,9 +506,6 @@ __global__ __launch_bounds__(NT, GCA_ALEX_WGS) void alex_step_kernel(
     if (wave_need) {
         load_vd();
         load_ps(0, psbuf[0]);  // first p_slope load: in flight during the prefix and heat phases
-#if GCA_ALEX_WGS < 4
-        load_ps(1, psbuf[1]);  // (3 workgroups per CU: the second one too)
-#endif
         if (ES) {
             const float* es = psE + lo;
             if (q == 15 && row_ok && cbase + 16 < W) {
@@ -641,8 +547,7 @@ __global__ __launch_bounds__(NT, GCA_ALEX_WGS) void alex_step_kernel(
         }
     }
     __syncthreads();
-    if (GCA_ALEX_PRIO >= 4) __builtin_amdgcn_s_setprio(GCA_ALEX_PRIO == 4 ? 1 : 0);  // past the last barrier
-    ALEX_STAMP(2);
+    __builtin_amdgcn_s_setprio(0);  // past the last barrier
 
     __builtin_amdgcn_sched_barrier(0);
 
@@ -661,7 +566,6 @@ __global__ __launch_bounds__(NT, GCA_ALEX_WGS) void alex_step_kernel(
     const float w_in_minus_bd = __fsub_rn(p.dous_inner, p.dous_border);
     auto fire_f = [](uint32_t s) -> float { return R <= 7 ? (float)(s & 0xFFu) : (float)(s & 0xFFFFu); };
     if (wave_need) {
-#ifndef GCA_ABL_NOHEAT
         // Window sums by lane-local prefix + DPP halo: lane q reads only its own 16 columns of the two
         // prefix rows (4 + 4 ds_read_b128), V = bottom - top; P = inclusive prefix of V over the 16
         // columns. The k columns left of the lane are the left lane's suffix T(m) = P(15) - P(15 - m)
@@ -733,37 +637,10 @@ __global__ __launch_bounds__(NT, GCA_ALEX_WGS) void alex_step_kernel(
             for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(ph2[j]), "+v"(dz2[j]));
             __builtin_amdgcn_sched_barrier(0);
         }
-#endif
 #pragma unroll
         for (int j = 0; j < 8; ++j) ph2[j] = ph2[j] - dz2[j];  // p_h = heat - dousing (:198)
-        if constexpr (!GL) {
-#if GCA_ALEX_WGS >= 4
-            load_ps(1, psbuf[1]);
-#endif
-        }
+        load_ps(1, psbuf[1]);
     }
-    if constexpr (GL) {
-        // retire every hipcc-visible load now, on every path (L0, vegetation / density, the edge values; hipcc
-        // cannot tell that the two `wave_need` branches agree, so a tie inside the first one would leave them
-        // pending on its fall-through path and hipcc would drain the hand-counted loads at their first use): from
-        // here on the slope loads are hand-counted and no hipcc wait may drain them
-#pragma unroll
-        for (int m = 0; m < 4; ++m)
-            asm volatile("" : "+v"(psbuf[0][m].x), "+v"(psbuf[0][m].y), "+v"(psbuf[0][m].z), "+v"(psbuf[0][m].w));
-        asm volatile("" : "+v"(e4), "+v"(e5), "+v"(e7), "+v"(vgw[0]), "+v"(vgw[1]), "+v"(vgw[2]), "+v"(vgw[3]),
-                     "+v"(dnw[0]), "+v"(dnw[1]), "+v"(dnw[2]), "+v"(dnw[3]));
-        // every wave's heat-phase reads of the prefix are done (their values are in registers) before the DMA
-        // overwrites it; a raw barrier: __syncthreads()' fence would add nothing hipcc knows to wait for here
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        if (wave_need) {
-            gl_ring(1, ring[1]);
-            gl_lds(2, 0);
-            gl_lds(3, 1);
-        }
-    }
-
-    ALEX_STAMP(3);
     // ---- FIRE bits of rows r-1, r, r+1: bit j of nbw[a] <-> staged column cc0 - 1 + j (j = 0..17)
     uint32_t nbw[3];
     fire_rows(nbw);
@@ -793,7 +670,7 @@ __global__ __launch_bounds__(NT, GCA_ALEX_WGS) void alex_step_kernel(
 #pragma unroll
     for (int j = 0; j < 8; ++j) qn2[j] = (f2){1.0f, 1.0f};
     uint32_t burn_inj = 0u;
-    if (GCA_ALEX_PRIO >= 3) __builtin_amdgcn_s_setprio(GCA_ALEX_PRIO == 3 ? 2 : 0);  // (A/B hook) slope-streaming pass
+    __builtin_amdgcn_s_setprio(0);  // (kept: it also fixes hipcc's schedule of the pass, measured r02r)
     if (wave_need) {
         // ---- base = (p_h * (1 + p_veg)) * (1 + p_den)   (left-to-right product of :206), clip(idx, 1, 5)
         //      (:176-178) through the LDS table
@@ -825,44 +702,10 @@ __global__ __launch_bounds__(NT, GCA_ALEX_WGS) void alex_step_kernel(
                                                              : (f2){psc[j >> 1].x, psc[j >> 1].y};
             } else {
                 float a[16];
-                if constexpr (GL) {
-                    // hand-counted waits: N = slope loads issued after the one consumed (issue order L1 | L2 L3
-                    // (DMA) | L4 after d0 | L5 after d1 | L6 (DMA) after d2); L0 was retired by hipcc
-                    if (d == 1)
-                        asm volatile("s_waitcnt vmcnt(12)" : "+v"(ring[1][0]), "+v"(ring[1][1]), "+v"(ring[1][2]),
-                                     "+v"(ring[1][3])::"memory");
-                    if (d == 2 || d == 3) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-                    if (d == 5)
-                        asm volatile("s_waitcnt vmcnt(8)" : "+v"(ring[0][0]), "+v"(ring[0][1]), "+v"(ring[0][2]),
-                                     "+v"(ring[0][3])::"memory");
-                    if (d == 6)
-                        asm volatile("s_waitcnt vmcnt(4)" : "+v"(ring[1][0]), "+v"(ring[1][1]), "+v"(ring[1][2]),
-                                     "+v"(ring[1][3])::"memory");
-                    if (d == 7) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    if (ld == 0) {
 #pragma unroll
-                        for (int i = 0; i < 16; ++i) {
-                            const float4 v = psbuf[0][i >> 2];
-                            a[i] = (i & 3) == 0 ? v.x : (i & 3) == 1 ? v.y : (i & 3) == 2 ? v.z : v.w;
-                        }
-                    } else if (ld == 1 || ld == 4 || ld == 5) {
-#pragma unroll
-                        for (int i = 0; i < 16; ++i) a[i] = ring[ld & 1][i >> 2][i & 3];
-                    } else {  // L2 / L6: slot 0, L3: slot 1
-                        const unsigned char* sl = smem + slot_off + 4096u * (ld == 3 ? 1u : 0u) + 16u * (uint32_t)(tid & 63);
-#pragma unroll
-                        for (int m = 0; m < 4; ++m) {
-                            const f4v v = *reinterpret_cast<const f4v*>(sl + 1024 * m);
-#pragma unroll
-                            for (int j = 0; j < 4; ++j) a[4 * m + j] = v[j];
-                        }
-                    }
-                } else {
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) {
-                        const float4 v = psc[i >> 2];
-                        a[i] = (i & 3) == 0 ? v.x : (i & 3) == 1 ? v.y : (i & 3) == 2 ? v.z : v.w;
-                    }
+                for (int i = 0; i < 16; ++i) {
+                    const float4 v = psc[i >> 2];
+                    a[i] = (i & 3) == 0 ? v.x : (i & 3) == 1 ? v.y : (i & 3) == 2 ? v.z : v.w;
                 }
                 // d = 4, 7: element i <- i + 1 (cell i's right / down-right neighbour);
                 // d = 5: element i <- i - 1; the row segment's outer element comes from the next /
@@ -934,14 +777,7 @@ __global__ __launch_bounds__(NT, GCA_ALEX_WGS) void alex_step_kernel(
             for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(qn2[j]));  // finish this direction's products here
             // refill the buffer just consumed with load ld + 2 (ES: not after d = 3, whose load d = 4 reuses)
             const int last = ES ? 6 : 7;
-            if constexpr (GL) {
-                if (d == 0) gl_ring(4, ring[0]);
-                if (d == 1) gl_ring(5, ring[1]);
-                if (d == 2) {  // slot 0 read (its values are in registers) before the DMA refills it
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                    gl_lds(6, 0);
-                }
-            } else if (ld + 2 <= last && !(ES && d == 3)) {
+            if (ld + 2 <= last && !(ES && d == 3)) {
                 load_ps(ld + 2, psc);
             }
             if (d == 6) load_ages();            // its buffer is free from here on
@@ -951,8 +787,6 @@ __global__ __launch_bounds__(NT, GCA_ALEX_WGS) void alex_step_kernel(
         load_ages();
     }
 
-    if (GCA_ALEX_PRIO == 3) __builtin_amdgcn_s_setprio(0);
-    ALEX_STAMP(4);
     // ---- draws: burn / grow masks and the packed new-fire ages NA (two cells per word)
     uint32_t burn, grow, NA[8];
     if (INJECT) {
@@ -982,11 +816,7 @@ __global__ __launch_bounds__(NT, GCA_ALEX_WGS) void alex_step_kernel(
             u32x4 XA = u32x4{0u, 0u, 0u, 0u}, XB = u32x4{0u, 0u, 0u, 0u};
             uint32_t m0, m1, a0, a1;
             if (!odd) {
-#ifdef GCA_ABL_NOPHILOX
-                if (nd) XA = u32x4{cA * 0x9E3779B9u, env_id ^ cA, step + cA, cA};
-#else
                 if (nd) XA = philox4x32_10(u32x4{cA, env_id, step, GCA_TAG_ALEX_CELL}, k0, k1);
-#endif
                 m0 = XA.x; a0 = XA.y; m1 = XA.z; a1 = XA.w;
             } else {
                 if (nd & 1u) XA = philox4x32_10(u32x4{cA, env_id, step, GCA_TAG_ALEX_CELL}, k0, k1);
@@ -1053,9 +883,7 @@ __global__ __launch_bounds__(NT, GCA_ALEX_WGS) void alex_step_kernel(
         nagew[pp] = bfi32(bm, NA[pp], a1);
     }
 
-    ALEX_STAMP(5);
     // ---------------- stores
-    if (GCA_ALEX_PRIO == 2 || GCA_ALEX_PRIO == 3) __builtin_amdgcn_s_setprio(3);  // (A/B hook) finish and free the slot
     if (vec) {
         uint8_t* gEo = grid_out + (size_t)e * HW;
         int16_t* aEo = age_out + (size_t)e * HW;
@@ -1072,7 +900,6 @@ __global__ __launch_bounds__(NT, GCA_ALEX_WGS) void alex_step_kernel(
         }
     }
     write_rgb(newT, newF);
-    ALEX_STAMP(6);
     if (counts || (PK && act_out)) {
         int cntT = __builtin_popcount(newT & okB), cntF = __builtin_popcount(newF & okB),
             cntE = __builtin_popcount(newE & okB);
@@ -1145,12 +972,8 @@ void dispatch_r(int R, const gca_alex_params& p, int E, int H, int W, const uint
 #define GCA_ALEX_CASE(RV) \
     case RV: launch_alex<RV, MODE, ES, PK, OBS>(p, E, H, W, gi, go, ai, ao, veg, den, dous, ps, wi, rs, ib, ig, ia, po, counts, st, act_in, act_out, obs); break;
     switch (R) {
-#ifdef GCA_ALEX_ONLY_R  // ISA inspection builds: one radius only
-        GCA_ALEX_CASE(GCA_ALEX_ONLY_R)
-#else
         GCA_ALEX_CASE(1) GCA_ALEX_CASE(2) GCA_ALEX_CASE(3) GCA_ALEX_CASE(4)
         GCA_ALEX_CASE(5) GCA_ALEX_CASE(6) GCA_ALEX_CASE(7) GCA_ALEX_CASE(8)
-#endif
     }
 #undef GCA_ALEX_CASE
 }
@@ -1276,11 +1099,6 @@ extern "C" int gca_alex_step_packed_rgb(const gca_alex_params* p, int E, int H, 
                                  AlexObs{reinterpret_cast<const float4*>(color_table), is_night, rgb}, stream);
 }
 
-#ifdef GCA_ALEX_STAMPS
-extern "C" int gca_debug_alex_stamps(unsigned long long* host_out) {
-    return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_alex_stamps), sizeof(g_alex_stamps)) == hipSuccess ? 0 : 2;
-}
-#endif
 
 // ------------------------------------------------------------------ packed env layers
 namespace {

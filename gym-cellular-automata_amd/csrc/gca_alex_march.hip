@@ -697,12 +697,8 @@ void dispatch_march(const gca_alex_params& p, int E, int H, const uint8_t* gi, u
 #define GCA_MARCH_CASE(RV) \
     case RV: launch_march<RV, OBS>(p, E, H, gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs, st); break;
     switch (p.R) {
-#ifdef GCA_ALEX_ONLY_R
-        GCA_MARCH_CASE(GCA_ALEX_ONLY_R)
-#else
         GCA_MARCH_CASE(1) GCA_MARCH_CASE(2) GCA_MARCH_CASE(3) GCA_MARCH_CASE(4)
         GCA_MARCH_CASE(5) GCA_MARCH_CASE(6) GCA_MARCH_CASE(7) GCA_MARCH_CASE(8)
-#endif
     }
 #undef GCA_MARCH_CASE
 }

@@ -4,7 +4,7 @@
 //            apply_extensions (bulldozer/utils/extension_utils.py:89-196), the reset observation
 //            (advanced_bulldozer.py:401-411).
 //
-// Grid: one workgroup (256 threads) per (env, block of up to GCA_OBS_RB = 32 rows):
+// Grid: one workgroup (256 threads) per (env, block of up to OBS_RB = 16 rows):
 //   A. (step mode, only when an extension channel can be non-zero) the first row holding a positive
 //      extension value — the reference's `has_extension` is a vmap over the ROWS of the channel-last
 //      (H, W, 3 + n_ext) stack, and the row index found is then used as the channel index (clamped to
@@ -24,28 +24,14 @@
 //   vis(v) = (v == 3 && !is_night) ? 0 : v   (the reference's literal 3, extension_utils.py:93).
 #include "gca_common.h"
 
-#ifndef GCA_OBS_DB
-#define GCA_OBS_DB 0  // 1: two RGB transposition buffers, one barrier per render round (A/B hook)
-#endif
-#ifndef GCA_OBS_WAVE
-#define GCA_OBS_WAVE 1  // wave-local RGB transposition (each wave stores its own 3 KiB), no barriers per round; 0: block-wide (r01p A/B: 0.713 vs 0.722 ms)
-#endif
-#ifndef GCA_OBS_RB
-#define GCA_OBS_RB 16  // rows per workgroup (r02f A/B at W = 256 with the wave-local transposition: 8 / 12 / 16 / 32 rows -> 0.84 / 0.70 / 0.64 / 0.70 ms; r01o block-wide: 16 / 32 -> 0.76 / 0.72)
-#endif
-#ifndef GCA_OBS_PRE
-#define GCA_OBS_PRE 5  // staged 16-B chunks per thread issued before the display scan (W = 256, 32 rows: 4.1 needed)
-#endif
-#ifndef GCA_OBS_BATCH
-#define GCA_OBS_BATCH 1  // full rounds: 3 LDS reads, one wait, 3 stores (A/B hook)
-#endif
-#ifndef GCA_OBS_PLAIN
-#define GCA_OBS_PLAIN 1  // chunks of 256 cells per wave in adv_obs_plain_kernel (0: always the staged kernel; r02k with
-                         // extensions off: 1 / 8 / 16 chunks -> 0.633 / 0.726 / 0.726 ms, staged kernel 0.688 ms)
-#endif
-#ifndef GCA_OBS_NT
-#define GCA_OBS_NT 1  // non-temporal RGB stores (r01i A/B: 1.07 vs 1.10 ms per 4096 x 256^2)
-#endif
+// Measured choices (the A/B variants were removed after the measurement):
+//   wave-local RGB transposition (each wave stores its own 3 KiB, no barriers per round; r01p: 0.713 vs 0.722 ms for
+//   the block-wide one, two block-wide buffers with one barrier per round 1.08 ms); non-temporal RGB stores (r01i:
+//   1.07 vs 1.10 ms); full rounds batched as 3 LDS reads, one wait, 3 stores
+constexpr int OBS_RB = 16;   // rows per workgroup (r02f at W = 256: 8 / 12 / 16 / 32 rows -> 0.84 / 0.70 / 0.64 / 0.70 ms)
+constexpr int OBS_PRE = 5;   // staged 16-B chunks per thread issued before the display scan (W = 256, 32 rows: 4.1)
+constexpr int OBS_PLAIN = 1; // chunks of 256 cells per wave in adv_obs_plain_kernel (r02k: 1 / 8 / 16 chunks ->
+                             // 0.633 / 0.726 / 0.726 ms, the staged kernel 0.688 ms)
 
 namespace {
 
@@ -149,7 +135,7 @@ __global__ __launch_bounds__(256) void adv_observation_kernel(gca_obs_params p, 
     for (int i = 0; i < p.n_ext; ++i) k.need_blur |= ((k.on >> i) & 1u) && !p.ext_skip_blur[i];
     const int nch = 3 + p.n_ext;
 
-    // ---- staging loads first (W % 16 == 0, 16-B aligned: the production shape): up to GCA_OBS_PRE 16-B
+    // ---- staging loads first (W % 16 == 0, 16-B aligned: the production shape): up to OBS_PRE 16-B
     //      chunks per thread go to registers now and to LDS after the display scan, so the scan's loads and
     //      these overlap instead of queueing one HBM round trip behind the other at the head of every block
     const bool stage_all = (W & 3) == 0;  // the 4-cells-per-thread path reads both arrays from LDS
@@ -167,9 +153,9 @@ __global__ __launch_bounds__(256) void adv_observation_kernel(gca_obs_params p, 
         const int r = min(max(r0 - 1 + lr, 0), H - 1);
         return idx < ng16 ? (int64_t)r * W + 16 * cq : dgap + (int64_t)r0 * W + 16 * (int64_t)(idx - ng16);
     };
-    uint4 pre[GCA_OBS_PRE];
+    uint4 pre[OBS_PRE];
 #pragma unroll
-    for (int j = 0; j < GCA_OBS_PRE; ++j) {  // unconditional loads of clamped chunks: pre stays in VGPRs
+    for (int j = 0; j < OBS_PRE; ++j) {  // unconditional loads of clamped chunks: pre stays in VGPRs
         const int idx = min((int)threadIdx.x + 256 * j, max(nst - 1, 0));
         pre[j] = nst ? *reinterpret_cast<const uint4*>(g + src16(idx)) : make_uint4(0u, 0u, 0u, 0u);
     }
@@ -239,11 +225,11 @@ __global__ __launch_bounds__(256) void adv_observation_kernel(gca_obs_params p, 
     if (do_stage) {
         if (fast16) {
 #pragma unroll
-            for (int j = 0; j < GCA_OBS_PRE; ++j) {
+            for (int j = 0; j < OBS_PRE; ++j) {
                 const int idx = (int)threadIdx.x + 256 * j;
                 if (idx < ng16 + nd16) reinterpret_cast<uint4*>(idx < ng16 ? T : D - 16 * ng16)[idx] = pre[j];
             }
-            for (int idx = (int)threadIdx.x + 256 * GCA_OBS_PRE; idx < ng16 + nd16; idx += 256)
+            for (int idx = (int)threadIdx.x + 256 * OBS_PRE; idx < ng16 + nd16; idx += 256)
                 reinterpret_cast<uint4*>(idx < ng16 ? T : D - 16 * ng16)[idx] =
                     *reinterpret_cast<const uint4*>(g + src16(idx));
         } else if (stage_all) {
@@ -279,11 +265,10 @@ __global__ __launch_bounds__(256) void adv_observation_kernel(gca_obs_params p, 
     if ((W & 3) == 0) {
         // 256 threads x 4 cells per round; the 12 floats of each thread go through LDS so that every store
         // instruction writes 1 KiB of contiguous RGB (the rows of a block are contiguous in HBM)
-        __shared__ float4 OUT4s[(GCA_OBS_DB ? 2 : 1) * 256 * 3];
+        __shared__ float4 OUT4s[256 * 3];
         const int wq = W >> 2;
-        int buf = 0;
         for (int base_q = 0; base_q < rows * wq; base_q += 256) {
-            float4* OUT4 = OUT4s + buf * (256 * 3);
+            float4* OUT4 = OUT4s;
             const int idx = base_q + (int)threadIdx.x;
             if (idx < rows * wq) {
                 const int lr = idx / wq, c0 = (idx - lr * wq) * 4, r = r0 + lr;
@@ -334,19 +319,15 @@ __global__ __launch_bounds__(256) void adv_observation_kernel(gca_obs_params p, 
                 OUT4[3 * threadIdx.x + 1] = make_float4(out[4], out[5], out[6], out[7]);
                 OUT4[3 * threadIdx.x + 2] = make_float4(out[8], out[9], out[10], out[11]);
             }
-#if GCA_OBS_WAVE
             // a wave's 64 threads own 256 consecutive cells = 3 KiB of contiguous RGB: the transposition stays
             // inside the wave (LDS operations of one wave complete in order), so no workgroup barrier
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#else
-            __syncthreads();
-#endif
             const int n4 = 3 * min(256, rows * wq - base_q);
             float4* dst = reinterpret_cast<float4*>(rgb + (e * HW + (int64_t)r0 * W + 4 * (int64_t)base_q) * 3);
             typedef float f4v __attribute__((ext_vector_type(4)));
-            if (GCA_OBS_BATCH && GCA_OBS_WAVE && GCA_OBS_NT && n4 == 768) {
+            if (n4 == 768) {
                 // a full round (all but a block's ragged last one): the three LDS reads issue back to back, one
                 // wait, then the three 1-KiB stores — not read / wait / store three times over
                 const int q0 = 192 * ((int)threadIdx.x >> 6) + ((int)threadIdx.x & 63);
@@ -357,26 +338,16 @@ __global__ __launch_bounds__(256) void adv_observation_kernel(gca_obs_params p, 
             } else
 #pragma unroll
             for (int j = 0; j < 3; ++j) {
-                const int q4 = GCA_OBS_WAVE ? 192 * ((int)threadIdx.x >> 6) + ((int)threadIdx.x & 63) + 64 * j
-                                            : (int)threadIdx.x + 256 * j;
+                const int q4 = 192 * ((int)threadIdx.x >> 6) + ((int)threadIdx.x & 63) + 64 * j;
                 if (q4 < n4) {
-#if GCA_OBS_NT
                     const float4 v = OUT4[q4];
                     __builtin_nontemporal_store((f4v){v.x, v.y, v.z, v.w}, reinterpret_cast<f4v*>(dst + q4));
-#else
-                    dst[q4] = OUT4[q4];
-#endif
                 }
             }
-            if (GCA_OBS_WAVE) {  // this round's LDS reads before the next round's writes (same wave)
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            } else if (GCA_OBS_DB) {
-                buf ^= 1;  // the next round writes the other buffer: the barrier above orders this round's reads
-            } else {
-                __syncthreads();
-            }
+            // this round's LDS reads before the next round's writes (same wave)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
     } else {
         for (int idx = threadIdx.x; idx < rows * W; idx += blockDim.x) {
@@ -441,13 +412,8 @@ __global__ __launch_bounds__(256) void adv_obs_plain_kernel(gca_obs_params p, in
     uint32_t gw[CW], dw[CW];
 #pragma unroll
     for (int i = 0; i < CW; ++i) {
-#ifdef GCA_OBS_ABL_NOREAD  // ablation (wrong results): no grid / dousing reads, the stores alone
-        gw[i] = (uint32_t)i;
-        dw[i] = 0u;
-#else
         gw[i] = *reinterpret_cast<const uint32_t*>(grid + 256 * (c0 + i) + 4 * lane);
         dw[i] = *reinterpret_cast<const uint32_t*>(dsrc + 256 * (c0 + i) + 4 * lane);
-#endif
     }
 #pragma unroll
     for (int i = 0; i < CW; ++i) {
@@ -542,7 +508,7 @@ extern "C" int gca_adv_observation(const gca_obs_params* p, int mode, int E, int
                   "adv_observation: rgb must be 16-B and grid/dousing 4-B aligned");
     // rows per block; (2 RB + 2) * W bytes of dynamic LDS (grid + dousing), at most 48 KiB
     const int64_t HW = (int64_t)H * W;
-    constexpr int CWP = GCA_OBS_PLAIN;  // chunks of 256 cells per wave
+    constexpr int CWP = OBS_PLAIN;  // chunks of 256 cells per wave
     if (CWP > 0 && mode == 0 && !p->enable_extensions && !p->should_transform && channels == nullptr &&
         HW % 256 == 0 && (HW / 256) % (CWP > 0 ? CWP : 1) == 0) {
         const int64_t chunks = (int64_t)E * (HW / 256);
@@ -553,7 +519,7 @@ extern "C" int gca_adv_observation(const gca_obs_params* p, int mode, int E, int
         GCA_CHECK_LAUNCH("adv_obs_plain");
         return GCA_OK;
     }
-    const int RB = max(1, min(GCA_OBS_RB, 24576 / W - 1));
+    const int RB = max(1, min(OBS_RB, 24576 / W - 1));
     const int bpe = (H + RB - 1) / RB;
     hipLaunchKernelGGL(adv_observation_kernel, dim3((unsigned)((int64_t)E * bpe)), dim3(256), (size_t)(2 * RB + 2) * W,
                        (hipStream_t)stream, *p, mode, H, W, RB, bpe, grid, dousing, pos, is_night, time_step, action,

@@ -20,9 +20,8 @@
 //    Reward/done counts of the new grid are fused (wave reduction + 3 atomics).
 #include "gca_common.h"
 
-#ifndef GCA_WINDY_AHEAD
-#define GCA_WINDY_AHEAD 1  // windy_fast_kernel: row chunks in flight ahead of the one being computed (2, 4, 8: slower, r01o A/B)
-#endif
+// windy_fast_kernel: row chunks in flight ahead of the one being computed (r01o: 2 / 4 / 8 measured slower than 1)
+constexpr int WINDY_AHEAD = 1;
 
 // ------------------------------------------------------------------ dir mask
 __global__ void windy_dirmask_kernel(const double* __restrict__ wind, int64_t wind_stride,
@@ -161,24 +160,24 @@ __global__ __launch_bounds__(256) void windy_fast_kernel(uint8_t* __restrict__ b
     const int Rprev = s0 - RPW + g;
     Row16 prv = classify(load_row(Rprev, g == RPW - 1), Tp, Fp, g == RPW - 1 && Rprev >= 0);
     Row16 cur = classify(load_row(chunk_row(0), true), Tp, Fp, chunk_row(0) < H);
-    uint4 ring[GCA_WINDY_AHEAD];  // ring[u] holds chunk t + 1 when t % AHEAD == u
+    uint4 ring[WINDY_AHEAD];  // ring[u] holds chunk t + 1 when t % AHEAD == u
 #pragma unroll
-    for (int u = 0; u < GCA_WINDY_AHEAD; ++u) ring[u] = load_row(chunk_row(u + 1), wanted(u + 1));
+    for (int u = 0; u < WINDY_AHEAD; ++u) ring[u] = load_row(chunk_row(u + 1), wanted(u + 1));
 
     const int lane_up = (lane - LPR) & 63, lane_dn = (lane + LPR) & 63;
     const int lane_l = (lane - 1) & 63, lane_r = (lane + 1) & 63;
     const bool has_l = q > 0, has_r = q < LPR - 1;
 
     int32_t cntT = 0, cntF = 0, cntV = 0;
-    for (int t0 = 0; t0 < nT; t0 += GCA_WINDY_AHEAD) {
+    for (int t0 = 0; t0 < nT; t0 += WINDY_AHEAD) {
 #pragma unroll
-    for (int u = 0; u < GCA_WINDY_AHEAD; ++u) {
+    for (int u = 0; u < WINDY_AHEAD; ++u) {
         const int t = t0 + u;
         if (t >= nT) break;  // wave-uniform
         const int Rc = chunk_row(t), Rn = chunk_row(t + 1);
         Row16 nxt = classify(ring[u], Tp, Fp, wanted(t + 1) && Rn < H);
         // refill the slot just consumed: the load AHEAD + 1 chunks ahead, issued before computing this chunk
-        ring[u] = load_row(chunk_row(t + 1 + GCA_WINDY_AHEAD), wanted(t + 1 + GCA_WINDY_AHEAD));
+        ring[u] = load_row(chunk_row(t + 1 + WINDY_AHEAD), wanted(t + 1 + WINDY_AHEAD));
 
         uint32_t up[4], dn[4];
 #pragma unroll
@@ -249,17 +248,10 @@ __global__ __launch_bounds__(256) void windy_fast_kernel(uint8_t* __restrict__ b
 // neighbours are then the lane's own previous / next row (registers: no cross-lane traffic at all) and the horizontal
 // ones the neighbour lanes' edge dwords, moved by DPP whole-wave shifts (wave_shr:1 / wave_shl:1, lanes 0 / 63 read 0 =
 // the grid's left / right border) instead of ds_bpermute. Each row's fire flags and their two column shifts are built
-// once and used by the three output rows that see them. Loads run GCA_WINDY_RD rows ahead (one dword per lane each, so
+// once and used by the three output rows that see them. Loads run WINDY_RD rows ahead (one dword per lane each, so
 // many rows fit in flight); row indices are clamped, not branched, so hipcc keeps the counted waits.
-#ifndef GCA_WINDY_ROWS
-#define GCA_WINDY_ROWS 1  // 0: the 16-cells-per-lane fast kernel for every W
-#endif
-#ifndef GCA_WINDY_RSH
-#define GCA_WINDY_RSH 16  // strip height per wave (r02j: 16 / 32 / 64 rows -> config 5 CA 105.9 / 109.7 / 110.5 us, config 2 equal)
-#endif
-#ifndef GCA_WINDY_RD
-#define GCA_WINDY_RD 8  // rows in flight ahead of the row being classified
-#endif
+constexpr int WINDY_RSH = 16;  // strip height per wave (r02j: 16 / 32 / 64 rows -> config 5 CA 105.9 / 109.7 / 110.5 us)
+constexpr int WINDY_RD = 8;    // rows in flight ahead of the row being classified
 
 template <int NW>
 struct RowRaw {
@@ -410,7 +402,7 @@ __global__ __launch_bounds__(256) void windy_rows_kernel(uint8_t* __restrict__ b
     if (steps && steps[env] <= pass) return;
     // the wave index is wave-uniform: readfirstlane keeps s0 and every row index in SGPRs
     const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const int s0 = (sblk * 4 + wave) * GCA_WINDY_RSH;
+    const int s0 = (sblk * 4 + wave) * WINDY_RSH;
     if (s0 >= H) return;
     const bool odd = parity && parity[env];
     const int64_t HW = (int64_t)H * W;
@@ -420,7 +412,7 @@ __global__ __launch_bounds__(256) void windy_rows_kernel(uint8_t* __restrict__ b
     // the env's direction mask, forced into an SGPR (a VGPR copy made hipcc rebuild some masks per row)
     const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane((int)dir_mask[env]);
     int32_t cntT = 0, cntF = 0, cntV = 0;
-    windy_rows_strip<NW, GCA_WINDY_RSH, GCA_WINDY_RD, STD>(S, Dst, s0, H, m, lofs, Ep, Tp, Fp, cntT, cntF, cntV);
+    windy_rows_strip<NW, WINDY_RSH, WINDY_RD, STD>(S, Dst, s0, H, m, lofs, Ep, Tp, Fp, cntT, cntF, cntV);
     if (counts) {
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) {
@@ -554,7 +546,7 @@ template <int NW>
 static void launch_rows(uint8_t* b0, uint8_t* b1, const uint8_t* parity, const int32_t* steps, int pass,
                         const uint8_t* dm, int E, int H, int empty, int tree, int fire, int32_t* counts,
                         hipStream_t st) {
-    const int strips = (H + GCA_WINDY_RSH - 1) / GCA_WINDY_RSH;
+    const int strips = (H + WINDY_RSH - 1) / WINDY_RSH;
     const int bpe = (strips + 3) / 4;
     if (empty == 0 && tree == 3 && fire == 25)
         hipLaunchKernelGGL((windy_rows_kernel<NW, true>), dim3((unsigned)((int64_t)E * bpe)), dim3(256), 0, st, b0, b1,
@@ -584,11 +576,7 @@ static void launch_fast(uint8_t* b0, uint8_t* b1, const uint8_t* parity, const i
     constexpr int RPW = 64 / LPR;
     // strip height: >= 32 rows when there is enough work, multiple of RPW
     const int64_t rows = (int64_t)E * H;
-#ifdef GCA_WINDY_SH
-    int SH = GCA_WINDY_SH;  // A/B hook (scripts/build_variant.sh)
-#else
     int SH = 32;
-#endif
     while (SH > RPW && rows / SH < 8192) SH >>= 1;
     if (SH < RPW) SH = RPW;
     SH = ((SH + RPW - 1) / RPW) * RPW;
@@ -610,7 +598,7 @@ extern "C" int gca_windy_step(uint8_t* buf0, uint8_t* buf1, const uint8_t* parit
     const bool aligned = ((((uintptr_t)buf0) | ((uintptr_t)buf1)) & 15u) == 0;
     const int LPR = W / 16;
     const bool fast = !force_exact && empty == 0 && aligned && (W % 16 == 0) && LPR >= 1 && LPR <= 64 && (64 % LPR) == 0;
-    if (fast && GCA_WINDY_ROWS && (W == 256 || W == 512)) {
+    if (fast && (W == 256 || W == 512)) {
         if (W == 256) launch_rows<1>(buf0, buf1, parity, steps, pass, dir_mask, E, H, empty, tree, fire, counts, st);
         else launch_rows<2>(buf0, buf1, parity, steps, pass, dir_mask, E, H, empty, tree, fire, counts, st);
         GCA_CHECK_LAUNCH("windy_rows");

@@ -41,7 +41,7 @@ class EpisodeStats:
         self.ret = torch.zeros(num_envs, dtype=torch.float32, device=device)
         self.len = torch.zeros(num_envs, dtype=torch.int32, device=device)
         self.group = group
-        self._gather = StatsGather(num_envs, device, group=group)
+        self._gather = None  # built on the first gather: the process group may not exist yet
 
     def update(self, reward, done):
         self.ret += reward.to(torch.float32)
@@ -56,7 +56,16 @@ class EpisodeStats:
     def gather(self, done, finished_ret, finished_len):
         """All ranks' (done u8, return f32, length i32), each (world, E) in rank order (views of a reused
         buffer, valid until the next gather on the same buffer)."""
+        if self._gather is None:
+            self._gather = StatsGather(self.ret.numel(), self.ret.device, group=self.group)
         return self._gather.gather(done, finished_ret, finished_len)
+
+
+def _dist_world(group):
+    """(world size, rank) of `group` as of now: (1, 0) without an initialised process group."""
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size(group), dist.get_rank(group)
+    return 1, 0
 
 
 class StatsGather:
@@ -70,27 +79,50 @@ class StatsGather:
     `buffers` payload / result pairs rotate so that an asynchronous gather never has its payload overwritten by
     the next pack (the pack waits for the gather that last used its buffer). With one rank the pack writes the
     result row directly: one launch, no collective.
+
+    The world size is read from torch.distributed on every call (a gather built before init_process_group, or
+    across a destroy / re-init, rebuilds its buffers instead of silently skipping the collective). `world` and
+    `collective` override both for tests: `collective(out_flat, payload, group=...)` stands in for
+    dist.all_gather_into_tensor (e.g. a device copy on one GPU, so the side-stream rotation runs on HIP streams
+    without a second rank).
     """
 
-    def __init__(self, num_envs, device, group=None, buffers=2, len_dtype=torch.int32):
-        E = int(num_envs)
-        self.E = E
+    def __init__(self, num_envs, device, group=None, buffers=2, len_dtype=torch.int32, world=None, collective=None):
+        self.E = int(num_envs)
         self.device = torch.device(device)
         self.group = group
-        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
-        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
-        self.pad = (-E) % 4
-        self.row = 9 * E + self.pad
+        self.buffers = int(buffers)
         self.len_dtype = len_dtype
+        self._world_override = None if world is None else int(world)
+        self._collective = collective if collective is not None else dist.all_gather_into_tensor
+        self.pad = (-self.E) % 4
+        self.row = 9 * self.E + self.pad
         self._zero_pad = torch.zeros(self.pad, dtype=torch.uint8, device=self.device)
-        self.out = [torch.zeros((self.world, self.row), dtype=torch.uint8, device=self.device) for _ in range(buffers)]
+        self.world = None
+        self.stream = None
+        self._build(*self._world_now())
+
+    def _world_now(self):
+        if self._world_override is not None:
+            return self._world_override, 0
+        return _dist_world(self.group)
+
+    def _build(self, world, rank):
+        if self.world is not None and self.device.type == "cuda":
+            for ev in self._events:  # a rebuild must not free buffers a side-stream gather still reads
+                if ev is not None:
+                    torch.cuda.current_stream(self.device).wait_event(ev)
+        self.world, self.rank = world, rank
+        self.out = [torch.zeros((world, self.row), dtype=torch.uint8, device=self.device)
+                    for _ in range(self.buffers)]
         # one rank: the pack writes the result row itself; several: a payload the collective reads
-        self.payload = [o[0] if self.world == 1 else torch.zeros(self.row, dtype=torch.uint8, device=self.device)
+        self.payload = [o[0] if world == 1 else torch.zeros(self.row, dtype=torch.uint8, device=self.device)
                         for o in self.out]
         self._views = [self._make_views(o) for o in self.out]
-        self._events = [None] * buffers
+        self._events = [None] * self.buffers
         self.k = 0
-        self.stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" and self.world > 1 else None
+        if self.device.type == "cuda" and world > 1 and self.stream is None:
+            self.stream = torch.cuda.Stream(self.device)
 
     def _make_views(self, o):
         E = self.E
@@ -103,16 +135,20 @@ class StatsGather:
         E = self.E
         if ret.dtype != torch.float32 or length.element_size() != 4 or done.element_size() != 1:
             raise ValueError("gather takes ret f32, a 4-byte length and a 1-byte done flag")
+        if ret.numel() != E or length.numel() != E or done.numel() != E:
+            raise ValueError(f"gather sized for {E} envs per rank")
+        world, rank = self._world_now()
+        if world != self.world or rank != self.rank:
+            self._build(world, rank)
         if length.dtype != self.len_dtype:
             self.len_dtype = length.dtype
             self._views = [self._make_views(o) for o in self.out]
-        if ret.numel() != E or length.numel() != E or done.numel() != E:
-            raise ValueError(f"gather sized for {E} envs per rank")
         k = self.k
         self.k = (k + 1) % len(self.out)
         on_cuda = self.device.type == "cuda"
         if on_cuda and self._events[k] is not None:  # the side stream's last gather of this buffer is done
             torch.cuda.current_stream(self.device).wait_event(self._events[k])
+            self._events[k] = None
         parts = [ret.reshape(-1).view(torch.uint8), length.reshape(-1).view(torch.uint8),
                  done.reshape(-1).view(torch.uint8)]
         if self.pad:
@@ -124,12 +160,12 @@ class StatsGather:
             if async_op and self.stream is not None:
                 self.stream.wait_stream(torch.cuda.current_stream(self.device))
                 with torch.cuda.stream(self.stream):
-                    dist.all_gather_into_tensor(flat, self.payload[k], group=self.group)
+                    self._collective(flat, self.payload[k], group=self.group)
                     event = torch.cuda.Event()
                     event.record(self.stream)
                 self._events[k] = event
             else:
-                dist.all_gather_into_tensor(flat, self.payload[k], group=self.group)
+                self._collective(flat, self.payload[k], group=self.group)
         d, r, ln = self._views[k]
         return (d, r, ln, event) if async_op else (d, r, ln)
 
@@ -138,11 +174,12 @@ _GATHERS = {}
 
 
 def all_gather_stats(done, ret, length, group=None):
-    """One all-gather of the per-env (done u8, return f32, length) of every rank: (world, E) views in rank order
-    (9 bytes per env on the wire), through a StatsGather kept per (E, device, group) — no per-call allocation.
-    The views are valid until the next call with the same shapes rotates back to their buffer."""
-    key = (done.numel(), str(done.device), id(group))
+    """One all-gather of the per-env (done u8, return f32, length) of every rank: (world, E) tensors in rank order
+    (9 bytes per env on the wire), through a StatsGather kept per (E, device, group) — the collective allocates
+    nothing; the results are fresh clones (the hot path that wants the reused views calls StatsGather directly).
+    The StatsGather re-reads the world size on every call, so a cached one follows a re-initialised group."""
+    key = (done.numel(), str(done.device), group)  # the group object itself: its id could be reused once freed
     g = _GATHERS.get(key)
     if g is None:
         g = _GATHERS[key] = StatsGather(done.numel(), done.device, group=group, len_dtype=length.dtype)
-    return g.gather(done, ret, length)
+    return tuple(x.clone() for x in g.gather(done, ret, length))

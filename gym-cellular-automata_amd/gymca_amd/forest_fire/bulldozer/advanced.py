@@ -127,9 +127,9 @@ class AdvancedForestFireBulldozerEnv:
         # packed layout extras: vd = min(veg, 7) | min(den, 7) << 4 and the dousing bits (u16 per 16 columns)
         self.vd = torch.zeros((E, H, W), dtype=torch.uint8, **kw) if slope_layout == "packed" else None
         self.dous_bits = torch.zeros((E, H * W // 16), dtype=torch.int16, **kw) if slope_layout == "packed" else None
-        # tile activity map of the packed step (16 x 256 tiles; ping-pong with the grid): tiles whose 3 x 3 tile
+        # tile activity map of the tiled packed step (16 x 256 tiles; ping-pong with the grid): tiles whose 3 x 3 tile
         # neighbourhood holds no fire are copied instead of stepped (exact: p_tree = 0 here); all ones = unknown.
-        # Opt-in: it makes a sparse state's step ~20% faster and a dense one ~3% slower
+        # Opt-in, tiled step only (the marching step derives the same from the grid)
         self.act = None
         self.set_tile_skip(tile_skip)
         self.wind_index = torch.zeros(E, dtype=torch.int32, **kw)
@@ -210,14 +210,18 @@ class AdvancedForestFireBulldozerEnv:
         self._pack_layers()
 
     def set_tile_skip(self, on):
-        """Switch the packed step's tile activity map on / off (the map restarts as "every tile active")."""
+        """Switch the packed step's tile activity map on / off (the map restarts as "every tile active"). The marching
+        step finds its quiet tiles from the grid itself (cheaper than keeping the map: 0.41 vs 0.51 ms per 4096 x 256^2
+        step from the reset state, BENCH r03), so there tile_skip keeps no map and changes nothing; the map serves the
+        tiled step (step_kernel="tiled")."""
         import torch
 
         E, H, W = self.num_envs, self.nrows, self.ncols
         if on and self.slope_layout != "packed":
             raise ValueError("tile skipping needs the packed layout (W % 256 == 0, H % 16 == 0)")
-        self.act = (torch.ones((2, E, (H // 16) * (W // 256)), dtype=torch.uint8, device=self.device) if on
-                    else None)
+        self.tile_skip = bool(on)
+        self.act = (torch.ones((2, E, (H // 16) * (W // 256)), dtype=torch.uint8, device=self.device)
+                    if on and not self.march else None)
 
     def _pack_layers(self):
         """vd and dousing bits of the packed layout from the u8 layers (no-op for the other layouts)."""
@@ -461,13 +465,22 @@ class AdvancedForestFireBulldozerEnv:
         if obs is not None:
             ctx = obs[1]
             pe = ctx.get("per_env_context", {})
+            # the slope source and the shared context first: a reference-layout slope switches the env to the
+            # 8-plane layout (dousing counts beyond 1 allowed), and adopted winds set the wind_index range
+            slope_src = self._slope_source(pe.get("slope"))
+            shared = self._shared_changes(ctx.get("shared_context"))
+            n_winds = len(shared["winds"]) if "winds" in shared else len(self._winds)
             src_of(pe.get("true_grid"), "true_grid", self.grid[self.cur], (0, 255))
             src_of(pe.get("fire_age"), "fire_age", self.age[self.cur], (-32768, 32767))
-            dous_hi = 1 if self.dous_bits is not None else 255
+            to_planes = slope_src is not None and slope_src[0] == "ref"
+            dous_hi = 1 if (self.dous_bits is not None and not to_planes) else 255
             src_of(pe.get("dousing_count"), "dousing_count", self.dousing, (0, dous_hi))
             src_of(pe.get("vegetation"), "vegetation", self.vegetation, (0, 255))
             src_of(pe.get("density"), "density", self.density, (0, 255))
-            src_of(pe.get("wind_index"), "wind_index", self.wind_index, (0, len(self._winds) - 1))
+            src_of(pe.get("wind_index"), "wind_index", self.wind_index, (0, n_winds - 1))
+            if "winds" in shared and not any(name == "wind_index" for name, _, _ in plan):
+                if int(self.wind_index.max().item()) >= n_winds:
+                    raise ValueError("winds: fewer wind matrices than the current wind indices need")
             src_of(pe.get("is_night"), "is_night", self.is_night, (0, 1))
             src_of(pe.get("time_step"), "time_step", self.time_step)
             src_of(pe.get("key"), "key", self.rng_step)
@@ -475,14 +488,12 @@ class AdvancedForestFireBulldozerEnv:
             src_of(ctx.get("time"), "time", self.accu)
             if obs[0] is not None and self.rgb is not None:
                 src_of(obs[0], "rgb", self.rgb)
-            slope_src = self._slope_source(pe.get("slope"))
             alt = pe.get("altitude")
             if alt is not None and not (self.altitude is not None and self._is_own(alt, self.altitude)):
                 a = alt if dev.is_device_tensor(alt) else torch.as_tensor(np.asarray(alt))
                 if tuple(a.shape) != (E, H, W):
                     raise ValueError(f"altitude: shape {tuple(a.shape)} is not ({E}, {H}, {W})")
                 altitude_src = a
-            shared = self._shared_changes(ctx.get("shared_context"))
         if info is not None:
             src_of(info.get("steps_elapsed"), "steps_elapsed", self.steps_elapsed)
             src_of(info.get("reward_accumulated"), "reward_accumulated", self.reward_accumulated)
@@ -578,10 +589,8 @@ class AdvancedForestFireBulldozerEnv:
     def _apply_shared(self, ch):
         import torch
 
-        if "winds" in ch:
+        if "winds" in ch:  # (the wind_index range was checked against these winds before anything was written)
             w = ch["winds"]
-            if len(w) <= int(self.wind_index.max().item()):
-                raise ValueError("winds: fewer wind matrices than the current wind indices need")
             self._winds = w
             self._winds_dev = torch.as_tensor(w, device=self.device)
             self.alex_params.n_winds = self.env_params.n_winds = len(w)

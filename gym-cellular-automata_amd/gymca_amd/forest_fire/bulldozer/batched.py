@@ -55,9 +55,13 @@ class BatchedForestFireBulldozerEnv:
         self.params = p
         max_t = max(p.t_move[a] for a in range(9)) + max(p.t_shoot[0], p.t_shoot[1]) + t_any
         self.max_passes = int(math.floor(1.0 + max_t))  # accu < 1 before the step
-        fusable = self.max_passes == 1 and W in (256, 512) and self._empty == 0
+        # gca_bulldozer_step_fused's contract: W = 256 / 512, one pass at most, empty == 0 < tree < fire (the closed-form
+        # rule's code ordering); anything else takes the three-kernel step
+        fusable = (self.max_passes == 1 and W in (256, 512) and self._empty == 0
+                   and self._empty < self._tree < self._fire)
         if fused and not fusable:
-            raise ValueError("fused=True needs W in (256, 512) and at most one CA pass per env step")
+            raise ValueError("fused=True needs W in (256, 512), at most one CA pass per env step and codes "
+                             "empty = 0 < tree < fire")
         self.fused = fusable if fused is None else bool(fused)
         kw = dict(device=self.device)
         self.buf = torch.zeros((2, E, H, W), dtype=torch.uint8, **kw)

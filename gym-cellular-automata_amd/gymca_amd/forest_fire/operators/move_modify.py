@@ -10,7 +10,7 @@ import numpy as np
 
 from ... import _backend
 from ... import _device as dev
-from ..._lib import BulldozerParams, call, call_cpu
+from ..._lib import BulldozerParams, GCAError, call, call_cpu
 from ...operator import Operator
 from ...spaces import Tuple
 
@@ -73,6 +73,10 @@ def _run_host(params, grid, action_pair, position, with_grid):
     call_cpu("gca_move_modify", params, p_act, p_pos, None, H, W, None, 1, None)  # Move
     if with_grid:  # Modify of the one cell under the new position (move_modify.py:84-94), written back in place
         r, c = int(pos[0, 0]), int(pos[0, 1])
+        if arr.ndim != 2 or not (0 <= r < H and 0 <= c < W):  # numpy would wrap a negative index: refuse like the C path
+            raise GCAError(f"gca_move_modify (host backend) failed: argument: move_modify: position ({r}, {c}) "
+                           f"outside the {H}x{W} grid" if arr.ndim == 2 else
+                           "gca_move_modify (host backend) failed: argument: the grid must be 2-D (one env)")
         v = int(arr[r, c])
         if not 0 <= v <= 255:
             raise ValueError("cell values must fit the u8 layout (0..255)")

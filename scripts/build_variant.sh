@@ -1,5 +1,5 @@
 #!/bin/bash
-# Build an A/B variant of libgca_hip.so with extra compiler flags (e.g. -DGCA_ALEX_WGS=3) into
+# Build an A/B variant of libgca_hip.so (extra compiler flags, or another source tree via VARIANT_SRC) into
 # gym-cellular-automata_amd/gymca_amd/_lib/variants/<name>.so; select it with GCA_LIB_PATH=<that path>.
 # Usage: bash scripts/build_variant.sh <name> <flags...>
 set -e

@@ -5,7 +5,8 @@
 
 Writes profiles/<tag>_kernel_stats.csv (the rocprofv3 --stats summary, verbatim),
 profiles/<tag>_summary.md (per-kernel averages of every collected counter) and updates
-profiles/pmc_traffic.json, which bench.py reads for roofline.traffic.
+profiles/pmc_traffic.json, which bench.py reads for roofline.traffic / valu_busy — keyed by the kernel's template
+instance and stamped with the sha of its sources (bench.py kernel_src_sha), so a later source change voids it.
 
 HBM bytes follow MI355X_MICROARCH.md's gfx950 correction: FETCH_SIZE (KB) counts 16-B
 coalesced reads at half their size (calibrated here on count_kernel: a 268 MB stream reads
@@ -19,6 +20,9 @@ import re
 import shutil
 import sys
 from collections import defaultdict
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import kernel_src_sha  # noqa: E402  (the repo root's bench.py: the same hash it checks)
 
 KERNELS = {"alex_step_kernel": "alex_step", "alex_march_kernel": "alex_march", "windy_fast_kernel": "windy_fast", "windy_exact_kernel": "windy_exact",
            "windy_rows_kernel": "windy_rows", "adv_obs_plain_kernel": "adv_obs_plain",
@@ -102,13 +106,16 @@ def main(prof_dir, tag, out_dir="profiles"):
             gr = sum(vals[s]["GRBM_GUI_ACTIVE"]) / len(vals[s]["GRBM_GUI_ACTIVE"])
             busy = va * 4 / (1024 * gr / 8)
             traffic.setdefault(s, {})["valu_busy"] = busy
+        if "SQ_INSTS_VALU" in vals[s]:  # VALU instructions issued per launch (all waves)
+            traffic.setdefault(s, {})["valu_insts"] = sum(vals[s]["SQ_INSTS_VALU"]) / len(vals[s]["SQ_INSTS_VALU"])
             lines.append(f"| {s} | VALU busy (SQ_ACTIVE_INST_VALU x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)) | {busy:.3f} |")
     with open(os.path.join(out_dir, f"{tag}_summary.md"), "w") as f:
         f.write("\n".join(lines) + "\n")
     tj = os.path.join(out_dir, "pmc_traffic.json")
     cur = json.load(open(tj)) if os.path.exists(tj) else {}
     for s, t in traffic.items():
-        cur[s] = dict(t, tag=tag, avg_us=dur.get(s, (0, None))[1])
+        # src_sha: the kernel's sources as profiled; bench.py reports these figures only for the same sources
+        cur[s] = dict(t, tag=tag, avg_us=dur.get(s, (0, None))[1], timed_avg_us=tm.get(s), src_sha=kernel_src_sha(s))
     with open(tj, "w") as f:
         json.dump(cur, f, indent=1, sort_keys=True)
     print("\n".join(lines))

@@ -1,0 +1,66 @@
+"""CPU: bench.py's roofline provenance — traffic / valu_busy come from the committed profile of the timed kernel
+(template instance AND source hash), never from another build's entry (VERDICT r03 "what's weak" 4)."""
+import json
+import os
+import shutil
+import sys
+import types
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench():
+    sys.path.insert(0, ROOT)
+    import bench
+
+    return bench
+
+
+def _tree(tmp_path):
+    for d in ("gym-cellular-automata_amd/csrc", "include", "profiles"):
+        (tmp_path / d).mkdir(parents=True)
+    for f in ("gca_alex_march.hip", "gca_alex_rule.h", "gca_common.h", "gca_alex.hip"):
+        shutil.copy(os.path.join(ROOT, "gym-cellular-automata_amd", "csrc", f), tmp_path / "gym-cellular-automata_amd/csrc" / f)
+    shutil.copy(os.path.join(ROOT, "include", "gca.h"), tmp_path / "include" / "gca.h")
+
+
+def test_headline_key_names_the_launched_template():
+    bench = _bench()
+    p = types.SimpleNamespace(R=6, p_tree=0.0)
+    env = types.SimpleNamespace(alex_params=p, march=True, slope_layout="packed")
+    assert bench.headline_kernel_key(env) == "alex_march<6, false, false>"
+    p.p_tree = 0.5
+    assert bench.headline_kernel_key(env) == "alex_march<6, false, true>"
+    env = types.SimpleNamespace(alex_params=types.SimpleNamespace(R=7, p_tree=0.0), march=False, slope_layout="packed")
+    assert bench.headline_kernel_key(env) == "alex_step<7, 0, true, true, true, false>"
+    env.slope_layout = "planes"
+    assert bench.headline_kernel_key(env) == "alex_step<7, 0, true, false, false, false>"
+
+
+def test_profile_entry_requires_the_same_sources(tmp_path, monkeypatch):
+    bench = _bench()
+    _tree(tmp_path)
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    key = "alex_march<6, false, false>"
+    sha = bench.kernel_src_sha(key)
+    assert sha and sha == bench.kernel_src_sha("alex_march<6, false, true>")  # one family, one source set
+    args = types.SimpleNamespace(envs=4096, size=256)
+    entry = {"bytes_per_launch": 7.0e9, "valu_busy": 0.9, "tag": "rX", "src_sha": sha}
+    (tmp_path / "profiles" / "pmc_traffic.json").write_text(json.dumps({key: entry, "alex_march<6, false>": {
+        "bytes_per_launch": 1.0, "tag": "old"}}))
+    e, info = bench.profile_entry(args, key)
+    assert e["bytes_per_launch"] == 7.0e9 and info["match"] and info["tag"] == "rX"
+    # another template instance of the same family: no entry -> null, never a neighbour's figures
+    e, info = bench.profile_entry(args, "alex_march<6, true, false>")
+    assert e is None and not info["match"]
+    # an entry without a source stamp (older profile) -> null
+    e, info = bench.profile_entry(args, "alex_march<6, false>")
+    assert e is None and "predates" in info["why"]
+    # the kernel's source changes after profiling -> null
+    with open(tmp_path / "gym-cellular-automata_amd/csrc/gca_alex_march.hip", "a") as f:
+        f.write("\n// changed\n")
+    e, info = bench.profile_entry(args, key)
+    assert e is None and info["profile_src_sha"] == sha and info["src_sha"] != sha
+    # not the profiled workload -> null
+    e, info = bench.profile_entry(types.SimpleNamespace(envs=1024, size=256), key)
+    assert e is None

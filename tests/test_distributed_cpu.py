@@ -19,8 +19,17 @@ def _free_port():
 def _worker(rank, world, port, q):
     import torch.distributed as dist
 
+    from gymca_amd.distributed import EpisodeStats, StatsGather
+
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    # built BEFORE the process group exists: they must gather across ranks once it does
+    pre, pre_stats = StatsGather(4, "cpu"), EpisodeStats(4, "cpu")
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    v = torch.full((4,), float(rank))
+    pd, pr, pl = pre.gather(torch.full((4,), rank, dtype=torch.uint8), v, v.to(torch.int32))
+    sd, sr, sl = pre_stats.gather(torch.full((4,), rank, dtype=torch.uint8), v, v.to(torch.int32))
+    late_ok = (tuple(pd.shape) == (world, 4) and pr[:, 0].tolist() == [float(r) for r in range(world)]
+               and tuple(sd.shape) == (world, 4) and sl[:, 0].tolist() == list(range(world)))
     off, n = shard(7, world, rank)
     done = torch.tensor([(off + i) % 2 for i in range(n)], dtype=torch.uint8)
     ret = torch.tensor([-(off + i) / 10 for i in range(n)], dtype=torch.float32)
@@ -33,8 +42,6 @@ def _worker(rank, world, port, q):
     d, r, l = all_gather_stats(done, ret, ln)
     assert d.shape == (world, E)  # (world, E) views of the gathered buffer
     # the reused StatsGather: no allocation and two ops (the pack, the collective) per call
-    from gymca_amd.distributed import StatsGather
-
     g = StatsGather(E, "cpu", len_dtype=torch.int32)
     g.gather(done, ret, ln)  # warm
     with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU], profile_memory=True) as prof:
@@ -55,7 +62,7 @@ def _worker(rank, world, port, q):
               and e.thread in main]
     q.put((rank, d.reshape(-1).tolist(), r.reshape(-1).tolist(), l.reshape(-1).tolist(),
            sorted({e.name for e in ops}), len([e for e in ops if e.name == "aten::cat"]), len(allocs),
-           gd.reshape(-1)[:n].tolist() if rank == 0 else None))
+           gd.reshape(-1)[:n].tolist() if rank == 0 else None, late_ok))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -79,8 +86,9 @@ def test_gloo_world2_all_gather_of_episode_stats():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for _, _, _, _, names, n_cat, n_alloc, _ in out:
+    for _, _, _, _, names, n_cat, n_alloc, _, late_ok in out:
         assert n_cat == 3 and n_alloc == 0, (names, n_cat, n_alloc)  # 3 calls: one pack each, nothing allocated
+        assert late_ok  # gathers built before init_process_group follow the group once it exists
         assert any("gather" in nm for nm in names), names
     res = {r: (d, ret, ln) for r, d, ret, ln, *_ in out}
     assert res[0] == res[1]

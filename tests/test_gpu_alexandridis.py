@@ -336,6 +336,66 @@ def test_full_size_config3_step_properties(device):
         assert np.array_equal(counts[e], ec[0])
 
 
+def test_full_size_config4_step_properties(device):
+    """BASELINE config 4 (AdvancedBulldozer 256^2 with the hidden foliage / altitude layers, 4096 envs) one step
+    through the env, the bench's layers (hidden_rng="philox": init_utils.py:10-116's recipe drawn on the device,
+    get_slope on the device): invariants on every env, and three sampled envs vs the C oracle bit for bit with their
+    own vegetation / density / slope layers (reference: advanced_bulldozer.py:182-204, ca_alexandridis_jax.py:321-424)."""
+    import torch
+    import torch.nn.functional as F
+
+    from gymca_amd import _device as dev
+    from gymca_amd._lib import call
+    from gymca_amd.forest_fire.bulldozer import AdvancedForestFireBulldozerEnv
+
+    E, N = 4096, 256
+    env = AdvancedForestFireBulldozerEnv(N, N, key=2, num_envs=E, use_hidden=True, device=device, hidden_rng="philox",
+                                         observation="grid")
+    assert env.slope_layout == "packed" and env.march
+    env.reset()
+    veg, den = env.vegetation.clone(), env.density.clone()
+    assert int(veg.min()) >= 1 and int(veg.max()) <= 5 and int(den.min()) >= 1 and int(den.max()) <= 5
+    assert int(veg.to(torch.int32).std(dim=(1, 2)).gt(0).sum()) > E // 2  # hidden layers, not constants
+    gen = torch.Generator(device=device).manual_seed(4)
+    u = torch.rand((E, N, N), device=device, generator=gen)
+    grid = torch.where(u < 0.1, 0, torch.where(u < 0.9, 1, 2)).to(torch.uint8)
+    del u
+    age = torch.where(grid == 2, torch.randint(1, 673, (E, N, N), device=device, generator=gen), 0).to(torch.int16)
+    env.set_state(grid=grid, fire_age=age, wind_index=torch.randint(0, 8, (E,), device=device, generator=gen))
+    g0, a0 = grid, age.clone()
+    env.ca_step()
+    g1, a1 = env.grid[env.cur], env.age[env.cur]
+    assert torch.all(g1[g0 == 0] == 0)  # p_tree = 0: nothing grows
+    assert torch.all(g1[(g0 == 2) & (a0 <= 1)] == 0) and torch.all(g1[(g0 == 2) & (a0 > 1)] == 2)
+    assert torch.equal(a1[g0 == 2].to(torch.int32), a0[g0 == 2].to(torch.int32) - 1)
+    # a TREE burns only next to a FIRE (Moore neighbourhood, zero padding); a TREE that stays keeps its age
+    fire_nb = F.max_pool2d((g0 == 2).to(torch.float16).unsqueeze(1), 3, stride=1, padding=1).squeeze(1) > 0
+    tree = g0 == 1
+    assert torch.all(g1[tree & ~fire_nb] == 1)
+    assert torch.all((g1[tree] == 1) | (g1[tree] == 2))
+    burnt = tree & (g1 == 2)
+    assert torch.all(a1[burnt] >= 576) and torch.all(a1[burnt] < 672)  # randint[floor(1.5 S), floor(1.75 S))
+    assert torch.equal(a1[tree & (g1 == 1)], a0[tree & (g1 == 1)])
+    assert int(burnt.sum()) > 0
+    counts = env.counts.cpu().numpy()
+    assert np.all(counts.sum(axis=1) == N * N)
+    ref_counts = torch.stack([(g1 == k).sum(dim=(1, 2)) for k in range(3)], dim=1).cpu().numpy()
+    assert np.array_equal(counts, ref_counts)
+    st = dev.stream_ptr(device)
+    for e in (0, 1777, 4095):
+        planes = torch.empty((1, 8, N, N), dtype=torch.float32, device=device)
+        alt = env.altitude[e:e + 1].contiguous()
+        call("gca_alex_slope_from_altitude", dev.ptr(alt), dev.ptr(planes), None, 1, N, N, st)
+        p = alex_c.params_from(env.alex_params)
+        p.env_offset = e  # the oracle steps one env: shift the Philox env id
+        eg, ea, ec, _ = alex_c.alex_step(p, g0[e:e + 1].cpu().numpy(), a0[e:e + 1].cpu().numpy(),
+                                         veg[e:e + 1].cpu().numpy(), den[e:e + 1].cpu().numpy(),
+                                         np.zeros((1, N, N), np.uint8), planes.cpu().numpy(),
+                                         env.wind_index[e:e + 1].cpu().numpy(), rng_step=np.zeros(1, np.uint32))
+        assert np.array_equal(g1[e].cpu().numpy(), eg[0]) and np.array_equal(a1[e].cpu().numpy(), ea[0])
+        assert np.array_equal(counts[e], ec[0])
+
+
 # ------------------------------------------------------------------ classic variant (row a8)
 @pytest.mark.parametrize("H,W,seed", [(16, 16, 0), (21, 37, 1), (64, 64, 2)])
 def test_classic_dropin_matches_classic_restatement(device, H, W, seed):

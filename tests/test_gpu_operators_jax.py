@@ -189,3 +189,37 @@ def test_stateless_step_refuses_before_writing(device):
         with pytest.raises(ValueError):
             env.stateless_step(np.zeros((E, 3), np.int64), o, info)
         assert bool((env.grid[env.cur] == g0).all()), key
+
+
+def test_stateless_step_winds_and_indices_validated_together(device):
+    """a larger wind table adopted together with indices into it is accepted; a smaller table than the
+    env's current indices need is refused BEFORE anything (grid, wind_index ...) is written; a reference-layout slope
+    adopted with dousing counts above 1 is accepted (the env moves to the 8-plane layout, where counts are bytes)."""
+    import torch
+
+    from gymca_amd.forest_fire.bulldozer import AdvancedForestFireBulldozerEnv
+
+    E, N = 2, 256
+    env = AdvancedForestFireBulldozerEnv(N, N, key=4, num_envs=E, use_hidden=False, device=device, observation="grid")
+    obs, info = env.reset()
+    w = winds()
+    big = np.concatenate([w, w[:4]], axis=0)  # 12 wind matrices
+    pe = dict(obs[1]["per_env_context"], wind_index=np.array([10, 11], np.int32))
+    o = (obs[0], dict(obs[1], per_env_context=pe, shared_context=dict(obs[1]["shared_context"], winds=big)))
+    env.stateless_step(np.zeros((E, 3), np.int64), o, info)
+    assert env.alex_params.n_winds == 12 and len(env._winds) == 12
+    # now a 4-matrix table while the env's indices are >= 4: refused, and the grid in the same call is not written
+    env.set_state(wind_index=np.array([10, 11], np.int32))
+    obs, info = env._obs(), env._info()
+    g0, wi0 = env.grid[env.cur].clone(), env.wind_index.clone()
+    pe = dict(obs[1]["per_env_context"], true_grid=np.zeros((E, N, N), np.float32))
+    o = (obs[0], dict(obs[1], per_env_context=pe, shared_context=dict(obs[1]["shared_context"], winds=w[:4])))
+    with pytest.raises(ValueError):
+        env.stateless_step(np.zeros((E, 3), np.int64), o, info)
+    assert torch.equal(env.grid[env.cur], g0) and torch.equal(env.wind_index, wi0) and env.alex_params.n_winds == 12
+    # a reference-layout slope with dousing counts of 2: accepted, on the planes layout
+    case = make_case(E, N, N, 21)
+    pe = dict(obs[1]["per_env_context"], slope=case["slope"], dousing_count=np.full((E, N, N), 2, np.int32))
+    o = (obs[0], dict(obs[1], per_env_context=pe))
+    env.stateless_step(np.zeros((E, 3), np.int64), o, info)
+    assert env.slope_layout == "planes" and int(env.dousing.max()) == 2

@@ -57,6 +57,21 @@ def test_host_move_modify_matches_reference_rows(golden, dtype):
         assert int((grid != 0).sum()) == int(after != 0)  # nothing else touched
 
 
+def test_host_modify_refuses_positions_outside_the_grid():
+    """Every host path refuses a caller's position outside the grid like the C and HIP gca_move_modify (GCA_ERR_ARG):
+    numpy indexing would wrap a negative index and modify the wrong cell. The large-grid path (int64,
+    above HOST_MAX_CELLS) and the small-grid copy path both."""
+    from gymca_amd import GCAError
+    from gymca_amd.forest_fire.operators import Modify
+
+    for shape in ((80, 80), (8, 8)):
+        for pos in ((-1, 5), (5, -1), (shape[0], 0), (0, shape[1])):
+            grid = np.full(shape, 3, dtype=np.int64)
+            with pytest.raises(GCAError):
+                Modify({3: 0}, backend="cpu")(grid, 1, np.array(pos))
+            assert (grid == 3).all()  # nothing written
+
+
 def test_host_modify_large_grid_touches_one_cell():
     """O(1): a 512x512 int64 grid is modified in place at one cell (no whole-grid copy)."""
     from gymca_amd.forest_fire.operators import Modify
