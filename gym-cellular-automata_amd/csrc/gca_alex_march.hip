@@ -1,4 +1,4 @@
-// gca_alex_march.hip — the Alexandridis CA step on the Advanced env's packed layout, marching form (W = 256).
+// gca_alex_march.hip — the Alexandridis CA step on the Advanced env's packed layout, marching form (W = 256 * NSEG).
 // Reference: PartiallyObservableForestFireJax._update_grid (ca_alexandridis_jax.py:321-424) with
 // _compute_burn_probability (:164-206): the rule, the f32 arithmetic in its order and the Philox draws of
 // alex_step_kernel's packed mode (gca_alex.hip), bit for bit; only the work mapping differs.
@@ -18,15 +18,22 @@
 // every slope byte is read once (the tiled kernel re-reads three planes of row r+1 through L2: 27.4 B/cell of
 // traffic against 23.1 algorithmic, profiles/pmc_traffic.json). Lane reads are 16 B / 4 B / 8 B at 16 / 4 / 8 B
 // strides: 1 KiB, 256 B, 512 B contiguous per wave instruction.
-// The edge halo of a 256-column segment is the grid's zero border (W = 256): lane 0's left and lane 63's right
+// The edge halo of a 256-column segment is the grid's zero border at W = 256: lane 0's left and lane 63's right
 // DPP neighbours read 0 (EMPTY / no dousing), and the border cells' slope factors are 1.
+// W = 256 * NSEG (NSEG = 2, 4: the reference's R = 7 grids at 512^2, R = 8 at 1024^2): one workgroup = the NSEG waves of
+// one 16-row strip, wave g marching segment g (columns 256g .. 256g + 255) in step with its neighbours. After each row's
+// running sums move, every wave's edge lanes (0, 1, 62, 63) post what the neighbour segment's edge lanes take by DPP
+// from across the boundary — V_1..V_R, the two dousing sums, the FIRE flags of rows r-1, r, r+1 and three raw edge-slope
+// values — into a per-row-parity LDS exchange, one barrier, and each wave reads its neighbours' values straight into the
+// `old` operand of its edge DPPs (lane 0 <- the left segment's lane 63 / 62, lane 63 <- the right segment's lane 0 / 1;
+// the grid's border reads a slot of zeros and slope 1.0). Nothing else changes: the same cells, the same arithmetic.
 #include "gca_alex_rule.h"
 
 #include <type_traits>
 
 namespace {
 
-constexpr int MW = 256;  // grid width (one segment per row)
+constexpr int MW = 256;  // segment width (one wave per segment of a row; W = MW * NSEG)
 constexpr int SH = 16;   // rows per wave = one tile of the activity map (gca.h: gca_alex_step_packed)
 
 struct MarchObs {
@@ -43,6 +50,13 @@ __device__ __forceinline__ uint32_t from_prev(uint32_t v) {  // lane l <- lane l
 __device__ __forceinline__ uint32_t from_next(uint32_t v) {  // lane l <- lane l+1
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x130, 0xF, 0xF, true);
 }
+// the same with a halo: the lane without a source keeps `old` (lane 0: the left segment's value, lane 63: the right's)
+__device__ __forceinline__ uint32_t from_prev_or(uint32_t old, uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x138, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint32_t from_next_or(uint32_t old, uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x130, 0xF, 0xF, false);
+}
 
 // byte mask of dword o (lane l+o, o in -2..2) inside the window of radius k around the lane's column j
 __host__ __device__ constexpr uint32_t win_mask(int o, int j, int k) {
@@ -58,15 +72,19 @@ __host__ __device__ constexpr bool win_full(int o, int j, int k) { return j - k 
 // B[j] = sum of the byte counts X over columns 4l+j-k .. 4l+j+k (k <= 8: lanes l-2 .. l+2), v_dot4_u32_u8 chains. The
 // dwords a window covers fully (always a run around the lane's own: {0}, {-1,0}, {0,1} or {-1,0,1} for k >= 2) are summed
 // once and shared by the four windows; the partial dwords are added with their byte masks (k = 6: 10 dot4 instead of 16)
-__device__ __forceinline__ void window4(uint32_t X, int k, uint32_t (&B)[4], uint32_t z = 0u) {
+// HALO (NSEG > 1): h1 / h2 are the dwords beyond the segment's edges (lane 0: left segment's lanes 63 / 62, lane 63:
+// right segment's lanes 0 / 1)
+template <bool HALO = false>
+__device__ __forceinline__ void window4(uint32_t X, int k, uint32_t (&B)[4], uint32_t z = 0u, uint32_t h1 = 0u,
+                                        uint32_t h2 = 0u) {
     uint32_t n[5] = {0u, 0u, X, 0u, 0u};
     if (k >= 1) {
-        n[1] = from_prev(X);
-        n[3] = from_next(X);
+        n[1] = HALO ? from_prev_or(h1, X) : from_prev(X);
+        n[3] = HALO ? from_next_or(h1, X) : from_next(X);
     }
     if (k >= 5) {
-        n[0] = from_prev(n[1]);
-        n[4] = from_next(n[3]);
+        n[0] = HALO ? from_prev_or(h2, n[1]) : from_prev(n[1]);
+        n[4] = HALO ? from_next_or(h2, n[3]) : from_next(n[3]);
     }
     constexpr uint32_t ONES = 0x01010101u;
     // which full runs the four windows use (compile-time after unrolling)
@@ -116,18 +134,28 @@ __device__ __forceinline__ i16x2 bitcast_i16x2(uint32_t v) { return __builtin_bi
 __device__ __forceinline__ u16x2 bitcast_u16x2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
 template <class T> __device__ __forceinline__ uint32_t bitcast_u32(T v) { return __builtin_bit_cast(uint32_t, v); }
 
-template <int R, bool OBS, bool GROW>  // GROW: p_tree > 0 (EMPTY cells draw too)
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void alex_march_kernel(
+// exchange items per edge lane (NSEG > 1): V_1..V_8, D_1, D_2, FIRE flags of rows r-1, r, r+1, two raw slopes, pad
+constexpr int XI = 16;
+constexpr int XS_ONE = 13, XS_TWO = 14;  // items holding raw slopes (1.0 in the border slots: factor 1)
+
+template <int R, bool OBS, bool GROW, int NSEG>  // GROW: p_tree > 0 (EMPTY cells draw too); W = 256 * NSEG
+__global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_waves_per_eu(3, 3))) void alex_march_kernel(
     gca_alex_params p, int H, int nwaves, const uint8_t* __restrict__ grid_in, uint8_t* __restrict__ grid_out,
     const int16_t* age_in, int16_t* age_out,  // no __restrict__: the env updates ages in place
     const uint8_t* __restrict__ vd, const uint16_t* __restrict__ dbits, const float* __restrict__ es,
     const int32_t* __restrict__ wind_index, const uint32_t* __restrict__ rng_step, int32_t* __restrict__ counts,
     const uint8_t* __restrict__ act_in, uint8_t* __restrict__ act_out, MarchObs obs) {
     constexpr int NF = 2 * R + 2;  // fire ring rows r-R-1 .. r+R
-    __shared__ float lut[4][16];
-    __shared__ float4 colw[4][8];
-    __shared__ float4 img[OBS ? 4 : 1][OBS ? 192 : 1];  // OBS: one RGB row (3 KiB) per wave
-    __shared__ uint32_t fring[4][2 * NF * 64];              // per wave: the fire ring, each row twice
+    constexpr bool HALO = NSEG > 1;
+    constexpr int WPB = HALO ? NSEG : 4;  // waves per workgroup: 4 independent tiles, or the NSEG segments of a strip
+    constexpr int W = MW * NSEG;
+    __shared__ float lut[WPB][16];
+    __shared__ float4 colw[WPB][8];
+    __shared__ float4 img[OBS ? WPB : 1][OBS ? 192 : 1];  // OBS: one RGB row (3 KiB) per wave
+    __shared__ uint32_t fring[WPB][2 * NF * 64];              // per wave: the fire ring, each row twice
+    // HALO: [row parity][segment + 1][edge lane 0, 1, 62, 63][item]; segments 0 and NSEG + 1 are the grid's border
+    __shared__ uint32_t xch[HALO ? 2 : 1][HALO ? NSEG + 2 : 1][4][HALO ? XI : 1];
+    __shared__ uint32_t qfl[HALO ? NSEG : 1];
 
     // the wave index in SGPRs: everything derived from it (env, rows, base pointers, wind) stays scalar
     const int tid = threadIdx.x, wl = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
@@ -136,14 +164,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     const int xcd = (int)blockIdx.x & 7, slot = (int)blockIdx.x >> 3;
     const int qn8 = nb >> 3, rn8 = nb & 7;
     const int lb = (xcd < rn8 ? xcd * (qn8 + 1) : rn8 * (qn8 + 1) + (xcd - rn8) * qn8) + slot;
-    const int wv = lb * 4 + wl;
-    if (wv >= nwaves) return;  // wave-uniform; no barrier follows
-    const int strips = H / SH;
-    // (env-major wave order: one env's tiles back to back. A tile-major order inside chunks of 128 / 256 / 512 envs,
-    //  meant to turn the tiles' shared halo rows into L2 hits, measured 5 / 8 / 12 % slower, profiles/r03p)
-    const int e = wv / strips, s = wv - e * strips;
+    int strips, e, s, g;
+    if constexpr (!HALO) {
+        const int wv = lb * 4 + wl;
+        if (wv >= nwaves) return;  // wave-uniform; no barrier follows
+        strips = H / SH;
+        // (env-major wave order: one env's tiles back to back. A tile-major order inside chunks of 128 / 256 / 512
+        //  envs, meant to turn the tiles' shared halo rows into L2 hits, measured 5 / 8 / 12 % slower, profiles/r03p)
+        e = wv / strips;
+        s = wv - e * strips;
+        g = 0;
+    } else {
+        if (lb * NSEG >= nwaves) return;  // workgroup-uniform: every barrier below is reached by all its waves or none
+        strips = H / SH;
+        e = lb / strips;
+        s = lb - e * strips;
+        g = wl;
+    }
     const int s0 = s * SH;
-    const uint32_t HW = (uint32_t)H * MW;
+    const uint32_t HW = (uint32_t)H * W;
     const uint8_t* gE = grid_in + (size_t)e * HW;
     uint8_t* gO = grid_out + (size_t)e * HW;
     const int16_t* aE = age_in + (size_t)e * HW;
@@ -151,8 +190,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     const uint8_t* vE = vd + (size_t)e * HW;
     const uint16_t* dE = dbits + (size_t)e * (HW >> 4);
     const float* sE = es + (size_t)e * 4 * HW;
-    const uint32_t lc = 4u * (uint32_t)lane;  // column of the lane's cell 0 (= its grid byte offset in a row)
-    const uint32_t lane_a = 2u * lc, lane_s = 4u * lc, lane_d = 2u * (uint32_t)(lane >> 2);  // ages, slopes, dousing
+    // column of the lane's cell 0 (= its grid byte offset in a row) and its dousing-bit word (u16) in a row
+    const uint32_t lc = HALO ? (uint32_t)(MW * g) + 4u * (uint32_t)lane : 4u * (uint32_t)lane;
+    const uint32_t ld16 = HALO ? lc >> 4 : (uint32_t)(lane >> 2);
+    const uint32_t lane_a = 2u * lc, lane_s = 4u * lc, lane_d = 2u * ld16;  // ages, slopes, dousing
     const uint32_t Fp = rep4((uint32_t)p.fire), Ep = rep4((uint32_t)p.empty), Tp = rep4((uint32_t)p.tree);
 
     if (lane < 16) lut[wl][lane] = gca_alex_lut_entry(p, lane);
@@ -162,10 +203,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
     auto graw = [&](int r) -> uint32_t {  // grid bytes of the lane's 4 cells in row r (EMPTY outside the grid)
-        return (r >= 0 && r < H) ? *reinterpret_cast<const uint32_t*>(gE + (uint32_t)r * MW + lc) : Ep;
+        return (r >= 0 && r < H) ? *reinterpret_cast<const uint32_t*>(gE + (uint32_t)r * W + lc) : Ep;
     };
     auto draw_bits = [&](int r) -> uint32_t {  // the u16 of dousing bits holding the lane's 4 cells
-        return (r >= 0 && r < H) ? (uint32_t)dE[(uint32_t)r * (MW / 16) + (uint32_t)(lane >> 2)] : 0u;
+        return (r >= 0 && r < H) ? (uint32_t)dE[(uint32_t)r * (W / 16) + ld16] : 0u;
     };
     auto dflags = [&](uint32_t w16) -> uint32_t { return gca_spread4(w16 >> (4 * (lane & 3))); };
     // RGB row r of the lane's 4 cells (kinds from the new TREE / FIRE nibbles, pre-step dousing flags) through the
@@ -190,7 +231,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             typedef float f4t __attribute__((ext_vector_type(4)));
-            float* row = obs.rgb + ((size_t)e * H + r) * (MW * 3);
+            float* row = obs.rgb + ((size_t)e * H + r) * (W * 3) + (HALO ? (size_t)(MW * 3) * g : 0);
             float4 v[3];
 #pragma unroll
             for (int t = 0; t < 3; ++t) v[t] = img[wl][64 * t + lane];
@@ -216,7 +257,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
 #pragma unroll
     for (int t = 0; t < NF - 1; ++t) g_init[t] = graw(s0 - R - 1 + t);
     bool quiet = false;
-    if (act_out && act_in) {
+    if (!HALO && act_out && act_in) {
         const uint8_t* A = act_in + (size_t)e * strips;
         quiet = !(A[s] | (s > 0 ? A[s - 1] : 0) | (s + 1 < strips ? A[s + 1] : 0));
     } else if constexpr (!GROW) {
@@ -231,20 +272,41 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
             quiet = __ballot(f != 0u) == 0ull;
         }
     }
+    if constexpr (HALO) {
+        // the strip is quiet only when every segment is (a FIRE in a neighbour segment's edge column can ignite this
+        // one): one consensus, so all waves of the workgroup take the same path through the barriers below. Wave 0
+        // also fills the border slots of the exchange (both parities): zero sums / flags, raw slope 1.0 (factor 1)
+        if (wl == 0) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int idx = 4 * lane + j;  // 256 = 2 parities x 2 border slots x 4 edge lanes x 16 items
+                const int item = idx & 15, li = (idx >> 4) & 3, sl = ((idx >> 6) & 1) ? NSEG + 1 : 0, pa = idx >> 7;
+                xch[pa][sl][li][item] = (item == XS_ONE || item == XS_TWO) ? 0x3F800000u : 0u;
+            }
+        }
+        if (lane == 0) qfl[wl] = quiet ? 1u : 0u;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+        uint32_t all = 1u;
+#pragma unroll
+        for (int w = 0; w < NSEG; ++w) all &= qfl[w];
+        quiet = all != 0u;
+    }
     if (quiet) {
         int cE = 0, cT = 0;
 #pragma unroll 4
         for (int i = 0; i < SH; ++i) {
             const int r = s0 + i;
-            const uint32_t o = (uint32_t)r * MW + lc;
-            const uint32_t g = *reinterpret_cast<const uint32_t*>(gE + o);
-            *reinterpret_cast<uint32_t*>(gO + o) = g;
+            const uint32_t o = (uint32_t)r * W + lc;
+            const uint32_t gw = *reinterpret_cast<const uint32_t*>(gE + o);
+            *reinterpret_cast<uint32_t*>(gO + o) = gw;
             if (age_in != age_out) *reinterpret_cast<uint2*>(aO + o) = *reinterpret_cast<const uint2*>(aE + o);
-            cE += __builtin_popcount(bytes_eq01(g, Ep));
-            cT += __builtin_popcount(bytes_eq01(g, Tp));
-            if (OBS) write_rgb_row(r, gca_eq_nib(g, Tp), 0u, dflags(draw_bits(r)));
+            cE += __builtin_popcount(bytes_eq01(gw, Ep));
+            cT += __builtin_popcount(bytes_eq01(gw, Tp));
+            if (OBS) write_rgb_row(r, gca_eq_nib(gw, Tp), 0u, dflags(draw_bits(r)));
         }
-        if (act_out && lane == 0) act_out[(size_t)e * strips + s] = 0;
+        if (act_out && lane == 0) act_out[((size_t)e * strips + s) * NSEG + g] = 0;
         if (counts) {
 #pragma unroll
             for (int off = 32; off > 0; off >>= 1) {
@@ -280,13 +342,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     // row r's own codes are re-read one row ahead (nOwn) although the ring saw them R rows earlier: a per-wave LDS ring
     // of the codes instead cuts the traffic by 1.0 B / cell (26.2 -> 25.2) but measured 0.6-2 % slower (r03q/r03r)
     uint32_t nG = graw(s0 + R), nD = draw_bits(s0 + 2), nOwn = graw(s0);
-    uint32_t nVD = *reinterpret_cast<const uint32_t*>(vE + (size_t)s0 * MW + lc);
-    uint2 nAge = *reinterpret_cast<const uint2*>(aE + (size_t)s0 * MW + lc);
+    uint32_t nVD = *reinterpret_cast<const uint32_t*>(vE + (size_t)s0 * W + lc);
+    uint2 nAge = *reinterpret_cast<const uint2*>(aE + (size_t)s0 * W + lc);
     float4 sc[4], sn[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        sc[k] = ldf4(sE + (size_t)k * HW + (size_t)s0 * MW + lc);
-        sn[k] = ldf4(sE + (size_t)k * HW + (size_t)min(s0 + 1, H - 1) * MW + lc);
+        sc[k] = ldf4(sE + (size_t)k * HW + (size_t)s0 * W + lc);
+        sn[k] = ldf4(sE + (size_t)k * HW + (size_t)min(s0 + 1, H - 1) * W + lc);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -302,8 +364,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     uint32_t Dv1 = dring[1] + dring[2] + dring[3];
     uint32_t Dv2 = dring[0] + Dv1 + dring[4];
 
-    // border columns 0 and 255 (lanes 0 / 63, elements 0 / 3): slope factor 1 (the rows 0 / H-1: kill_row below)
-    const bool col_lo = lane == 0, col_hi = lane == 63;
+    // border columns 0 and W-1 (lanes 0 / 63 of the first / last segment, elements 0 / 3): slope factor 1 (the rows
+    // 0 / H-1: kill_row below)
+    const bool col_lo = lane == 0 && (!HALO || g == 0), col_hi = lane == 63 && (!HALO || g == NSEG - 1);
+    // HALO: the lane's read offset into a parity of the exchange: lane 63 reads the right segment's lane 0 (and 1),
+    // every other lane the left segment's lane 63 (and 62) — only lane 0's value is used; the rest read it broadcast
+    const uint32_t xo1 = HALO ? (lane == 63 ? (uint32_t)(((g + 2) * 4 + 0) * XI) : (uint32_t)((g * 4 + 3) * XI)) : 0u;
+    const uint32_t xo2 = HALO ? (lane == 63 ? (uint32_t)(((g + 2) * 4 + 1) * XI) : (uint32_t)((g * 4 + 2) * XI)) : 0u;
     // row s0's own factors of planes 0..2 (row r's directions 0..2 read prepared own factors; plane 3 stays raw)
     auto prep_own = [&](float4& v) {
         const gca_f2 a = gca_edge_factors_own(v.x, v.y), b = gca_edge_factors_own(v.z, v.w);
@@ -347,7 +414,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     // one row of the tile. SC: row r's planes (0..2 as prepared own factors, 3 raw); SN: row r+1's raw planes.
     // After the row, SN holds row r+1's prepared planes and SC row r+2's raw planes (loaded once direction 4 has
     // read SC): the caller swaps the roles.
-    auto row = [&](const int i, float4 (&SC)[4], float4 (&SN)[4]) {
+    auto row = [&](const int i, float4 (&SC)[4], float4 (&SN)[4], auto parity) {
         const int r = s0 + i;
         // ---- this row's inputs (loaded one row ago); issue row r+1's (rows clamped into the grid: the last row's
         //      loads are unused, and unconditional loads keep the two rows of the loop body branch-free)
@@ -357,12 +424,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
            //  measured 2.5 % slower, profiles/r03n/ab_buffer_loads.txt)
             const int rg = r + 1 + R, rd = r + 3;
             const uint32_t r1 = (uint32_t)min(r + 1, H - 1);
-            const uint32_t g = ld_at<uint32_t>(gE + (size_t)min(rg, H - 1) * MW, lc);
-            const uint32_t d = ld_at<uint16_t>(dE + (size_t)min(rd, H - 1) * (MW / 16), lane_d);
-            nOwn = ld_at<uint32_t>(gE + (size_t)r1 * MW, lc);
-            nVD = ld_at<uint32_t>(vE + (size_t)r1 * MW, lc);
-            nAge = ld_at<uint2>(aE + (size_t)r1 * MW, lane_a);
-            nG = rg < H ? g : Ep;
+            const uint32_t gl = ld_at<uint32_t>(gE + (size_t)min(rg, H - 1) * W, lc);
+            const uint32_t d = ld_at<uint16_t>(dE + (size_t)min(rd, H - 1) * (W / 16), lane_d);
+            nOwn = ld_at<uint32_t>(gE + (size_t)r1 * W, lc);
+            nVD = ld_at<uint32_t>(vE + (size_t)r1 * W, lc);
+            nAge = ld_at<uint2>(aE + (size_t)r1 * W, lane_a);
+            nG = rg < H ? gl : Ep;
             nD = rd < H ? d : 0u;
         }
         // Row r+2's slope planes (loaded during this row) serve rows r+1 and r+2, which can only need them with a FIRE
@@ -377,7 +444,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
             const uint32_t rs3 = i + 2 < SH ? rs : (uint32_t)s0;
 #pragma unroll
             for (int k = 0; k < 4; ++k)
-                SC[k] = ld_at<float4>(sE + (size_t)k * HW + (size_t)(k == 3 ? rs3 : rs) * MW, lane_s);
+                SC[k] = ld_at<float4>(sE + (size_t)k * HW + (size_t)(k == 3 ? rs3 : rs) * W, lane_s);
         };
         // ---- fire ring: row r+R enters; the running vertical sums move to row r
         uint32_t* Fb = FR + (NF - 1 - (uint32_t)i % NF) * 64;  // slot of row r+R; row r+R-t at slot + t
@@ -406,25 +473,62 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
         Dv1 += dring[4] - dring[1];
         Dv2 += dring[5] - dring[0];
 
+        // ---- HALO: post this row's edge values for the neighbour segments, one barrier, and read theirs. xr / xr2:
+        //      the neighbours' items (lane 0: left segment's lanes 63 / 62; lane 63: right segment's lanes 0 / 1).
+        //      Raw slopes posted: lane 0 the plane 3 value of (r, first column) and plane 0 of (r+1, first column),
+        //      lane 63 plane 2 of (r+1, last column) — what the neighbour's directions 4 / 7 and 5 read across the edge
+        //      (if the neighbour needs one, its cell there burns, so this wave loaded real planes: need_next above)
+        const uint32_t* xr = nullptr;
+        const uint32_t* xr2 = nullptr;
+        uint32_t hfm1 = 0u, hf0 = 0u, hfp1 = 0u;
+        if constexpr (HALO) {
+            constexpr int PAR = decltype(parity)::value;
+            if (lane < 2 || lane >= 62) {
+                const int xl = lane < 2 ? lane : lane - 60;
+                uint4* xd = reinterpret_cast<uint4*>(&xch[PAR][g + 1][xl][0]);
+                uint32_t vv[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) vv[k] = k + 1 <= R ? V[k + 1] : 0u;
+                const uint32_t sA = lane < 32 ? __float_as_uint(SC[3].x) : __float_as_uint(SN[2].w);
+                xd[0] = make_uint4(vv[0], vv[1], vv[2], vv[3]);
+                xd[1] = make_uint4(vv[4], vv[5], vv[6], vv[7]);
+                xd[2] = make_uint4(Dv1, Dv2, fm1, f0);
+                xd[3] = make_uint4(fp1, sA, __float_as_uint(SN[0].x), 0u);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+            xr = &xch[PAR][0][0][0] + xo1;
+            xr2 = &xch[PAR][0][0][0] + xo2;
+            hfm1 = xr[10];
+            hf0 = xr[11];
+            hfp1 = xr[12];
+        }
+
         // ---- masks of the row: own kinds, FIRE neighbourhood (3 rows x 6 columns per lane)
         const uint32_t treeB = gca_eq_nib(own, Tp), emptyB = gca_eq_nib(own, Ep);
         // burning-neighbour masks: 0xFF in byte j iff cell j's neighbour d is FIRE, from the row dwords shifted one
         // column across lanes ([prev.b3, X.b0..b2] / [X.b1..b3, next.b0]); built per direction inside the pass (8
         // live masks cost registers), and masked into the products with one SDWA v_and per cell
-        auto shl_c = [](uint32_t x) { return __builtin_amdgcn_alignbyte(x, from_prev(x), 3); };  // column c-1
-        auto shr_c = [](uint32_t x) { return __builtin_amdgcn_alignbyte(from_next(x), x, 1); };  // column c+1
+        auto shl_c = [](uint32_t x, uint32_t h) {  // column c-1 (HALO: lane 0's from the left segment)
+            return __builtin_amdgcn_alignbyte(x, HALO ? from_prev_or(h, x) : from_prev(x), 3);
+        };
+        auto shr_c = [](uint32_t x, uint32_t h) {  // column c+1 (HALO: lane 63's from the right segment)
+            return __builtin_amdgcn_alignbyte(HALO ? from_next_or(h, x) : from_next(x), x, 1);
+        };
         auto dir_mask = [&](int d) -> uint32_t {
             const uint32_t row = d < 3 ? fm1 : (d < 5 ? f0 : fp1);
+            const uint32_t hrow = d < 3 ? hfm1 : (d < 5 ? hf0 : hfp1);
             const int dc = d < 3 ? d - 1 : (d == 3 ? -1 : (d == 4 ? 1 : d - 6));
-            uint32_t m = dc < 0 ? shl_c(row) : (dc > 0 ? shr_c(row) : row);
+            uint32_t m = dc < 0 ? shl_c(row, hrow) : (dc > 0 ? shr_c(row, hrow) : row);
             m *= 0xFFu;
             asm volatile("" : "+v"(m));  // opaque: hipcc would fold the byte extractions into per-byte multiplies
             return m;
         };
         const uint32_t fireB = (f0 * 0x01020408u) >> 24;
         // a FIRE anywhere in the 3 x 3 block (the centre too: it only matters for TREE cells, which are not FIRE)
-        const uint32_t vor = fm1 | f0 | fp1;
-        const uint32_t anyfire = (((vor | shl_c(vor) | shr_c(vor)) & 0x01010101u) * 0x01020408u) >> 24;
+        const uint32_t vor = fm1 | f0 | fp1, hvor = hfm1 | hf0 | hfp1;
+        const uint32_t anyfire = (((vor | shl_c(vor, hvor) | shr_c(vor, hvor)) & 0x01010101u) * 0x01020408u) >> 24;
         gca_f2 qn[2] = {{1.0f, 1.0f}, {1.0f, 1.0f}};
         const bool row_need = __ballot((treeB & anyfire) != 0u) != 0ull;
         const bool kill_row = r == 0 || r == H - 1;       // every factor of row r is 1
@@ -457,7 +561,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
 #pragma unroll
                     for (int j = 0; j < 4; ++j) B[j] = (f0 >> (8 * j)) & 0xFFu;
                 } else {
-                    window4(V[k], k, B, WZ);
+                    if constexpr (HALO)
+                        window4<true>(V[k], k, B, WZ, xr[k - 1], k >= 5 ? xr2[k - 1] : 0u);
+                    else
+                        window4(V[k], k, B, WZ);
                 }
 #pragma unroll
                 for (int h = 0; h < 2; ++h)
@@ -468,8 +575,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
                 __builtin_amdgcn_sched_barrier(0);
             }
             uint32_t D1[4], D2[4];
-            window4(Dv1, 1, D1, WZ);
-            window4(Dv2, 2, D2, WZ);
+            if constexpr (HALO) {
+                window4<true>(Dv1, 1, D1, WZ, xr[8]);
+                window4<true>(Dv2, 2, D2, WZ, xr[9]);
+            } else {
+                window4(Dv1, 1, D1, WZ);
+                window4(Dv2, 2, D2, WZ);
+            }
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 gca_f2 dz = (gca_f2){w_in_minus_bd, w_in_minus_bd} * wsum_f2(D1[2 * h], D1[2 * h + 1]);
@@ -509,6 +621,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
                     __builtin_amdgcn_sched_barrier(0);
                 };
                 const float one[4] = {1.0f, 1.0f, 1.0f, 1.0f};
+                // HALO: the neighbour factors across the segment's edges (lane 63: planes 3 of (r, c+1) and 0 of
+                // (r+1, c+1) for directions 4 / 7; lane 0: plane 2 of (r+1, c-1) for direction 5), from the raw values
+                // the neighbour segments posted; at the grid's border the posted raw 1.0 gives factor 1
+                uint32_t h45 = 0x3F800000u, h7 = 0x3F800000u;
+                if constexpr (HALO && !KILL) {
+                    gca_f2 o_, n_;
+                    gca_edge_factors_both(__uint_as_float(xr[XS_ONE]), __uint_as_float(xr[XS_TWO]), o_, n_);
+                    h45 = __float_as_uint(n_.x);
+                    h7 = __float_as_uint(n_.y);
+                }
 #pragma unroll
                 for (int d = 0; d < 3; ++d) {  // prepared own factors of planes 0..2
                     const float a[4] = {SC[d].x, SC[d].y, SC[d].z, SC[d].w};
@@ -523,9 +645,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
                     gca_edge_factors_both(SC[3].z, SC[3].w, ob, nb2);
                     const float a3[4] = {col_lo ? 1.0f : oa.x, oa.y, ob.x, col_hi ? 1.0f : ob.y};
                     apply(3, a3);
-                    // (r, c+1)'s plane 3; lane 63's last cell is column 255 (DPP old = 1.0)
+                    // (r, c+1)'s plane 3; lane 63's last cell is column 255 (DPP old = 1.0; HALO: the right segment's)
                     const float nx = __uint_as_float((uint32_t)__builtin_amdgcn_update_dpp(
-                        (int)0x3F800000u, (int)__float_as_uint(na.x), 0x130, 0xF, 0xF, false));
+                        (int)h45, (int)__float_as_uint(na.x), 0x130, 0xF, 0xF, false));
                     const float a4[4] = {col_lo ? 1.0f : na.y, nb2.x, nb2.y, nx};
                     apply(4, a4);
                 }
@@ -537,7 +659,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
                     apply(5, one);
                 } else {
                     const float pv = __uint_as_float((uint32_t)__builtin_amdgcn_update_dpp(
-                        (int)0x3F800000u, (int)__float_as_uint(nb[3]), 0x138, 0xF, 0xF, false));
+                        (int)h45, (int)__float_as_uint(nb[3]), 0x138, 0xF, 0xF, false));
                     const float a5[4] = {pv, nb[0], nb[1], col_hi ? 1.0f : nb[2]};
                     apply(5, a5);
                 }
@@ -555,7 +677,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
                     apply(7, one);
                 } else {
                     const float nx = __uint_as_float((uint32_t)__builtin_amdgcn_update_dpp(
-                        (int)0x3F800000u, (int)__float_as_uint(nb[0]), 0x130, 0xF, 0xF, false));
+                        (int)h7, (int)__float_as_uint(nb[0]), 0x130, 0xF, 0xF, false));
                     const float a7[4] = {col_lo ? 1.0f : nb[1], nb[2], nb[3], nx};
                     apply(7, a7);
                 }
@@ -572,7 +694,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
 
         // ---- draws: one Philox block per cell pair (cells 4l, 4l+1 and 4l+2, 4l+3), as gca_alex.hip
         const uint32_t needB = (treeB & anyfire) | (GROW ? emptyB : 0u);
-        const uint32_t lin0 = (uint32_t)r * MW + lc;
+        const uint32_t lin0 = (uint32_t)r * W + lc;
         uint32_t burn = 0u, grow = 0u, NA[2];
         // every lane draws when any lane of the wave needs to (a wave-uniform branch instead of a masked one per
         // pair): the draws of cells that need none are discarded (qn = 1 gives thr = 0; grow is masked by EMPTY)
@@ -633,7 +755,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
             const uint32_t bm = (((burn >> (2 * h)) & 1u) * 0xFFFFu) | (((burn >> (2 * h + 1)) & 1u) * 0xFFFF0000u);
             nag[h] = gca_bfi32(bm, NA[h], a1);
         }
-        const size_t o = (size_t)r * MW + lc;
+        const size_t o = (size_t)r * W + lc;
         *reinterpret_cast<uint32_t*>(gO + o) = outw;
         *reinterpret_cast<uint2*>(aO + o) = make_uint2(nag[0], nag[1]);
         write_rgb_row(r, newT, newF, dring[3]);
@@ -646,13 +768,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     };
 #pragma unroll 1
     for (int i = 0; i < SH; i += 2) {
-        row(i, sc, sn);
-        row(i + 1, sn, sc);
+        row(i, sc, sn, std::integral_constant<int, 0>{});
+        row(i + 1, sn, sc, std::integral_constant<int, 1>{});
     }
 
     if (counts || act_out) {
         const bool anyF = __ballot(cntF != 0) != 0ull;
-        if (act_out && lane == 0) act_out[(size_t)e * strips + s] = anyF ? 1 : 0;
+        if (act_out && lane == 0) act_out[((size_t)e * strips + s) * NSEG + g] = anyF ? 1 : 0;
         if (counts) {
 #pragma unroll
             for (int off = 32; off > 0; off >>= 1) {
@@ -669,33 +791,49 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     }
 }
 
+template <int R, bool OBS, bool GROW, int NSEG>
+void launch_march_n(const gca_alex_params& p, int E, int H, const uint8_t* gi, uint8_t* go, const int16_t* ai,
+                    int16_t* ao, const uint8_t* vd, const uint16_t* db, const float* es, const int32_t* wi,
+                    const uint32_t* rs, int32_t* counts, const uint8_t* act_in, uint8_t* act_out, MarchObs obs,
+                    hipStream_t st) {
+    const int nwaves = E * (H / SH) * NSEG;
+    if constexpr (NSEG == 1)  // four independent tiles per workgroup
+        hipLaunchKernelGGL((alex_march_kernel<R, OBS, GROW, 1>), dim3((unsigned)((nwaves + 3) / 4)), dim3(256), 0, st, p,
+                           H, nwaves, gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs);
+    else  // one strip (NSEG segment waves) per workgroup
+        hipLaunchKernelGGL((alex_march_kernel<R, OBS, GROW, NSEG>), dim3((unsigned)(nwaves / NSEG)), dim3(64 * NSEG), 0,
+                           st, p, H, nwaves, gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs);
+}
 template <int R, bool OBS, bool GROW>
-void launch_march_g(const gca_alex_params& p, int E, int H, const uint8_t* gi, uint8_t* go, const int16_t* ai,
-                  int16_t* ao, const uint8_t* vd, const uint16_t* db, const float* es, const int32_t* wi,
-                  const uint32_t* rs, int32_t* counts, const uint8_t* act_in, uint8_t* act_out, MarchObs obs,
-                  hipStream_t st) {
-    const int nwaves = E * (H / SH);
-    hipLaunchKernelGGL((alex_march_kernel<R, OBS, GROW>), dim3((unsigned)((nwaves + 3) / 4)), dim3(256), 0, st, p, H, nwaves,
-                       gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs);
+void launch_march_g(const gca_alex_params& p, int E, int H, int W, const uint8_t* gi, uint8_t* go, const int16_t* ai,
+                    int16_t* ao, const uint8_t* vd, const uint16_t* db, const float* es, const int32_t* wi,
+                    const uint32_t* rs, int32_t* counts, const uint8_t* act_in, uint8_t* act_out, MarchObs obs,
+                    hipStream_t st) {
+    if (W == MW)
+        launch_march_n<R, OBS, GROW, 1>(p, E, H, gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs, st);
+    else if (W == 2 * MW)
+        launch_march_n<R, OBS, GROW, 2>(p, E, H, gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs, st);
+    else
+        launch_march_n<R, OBS, GROW, 4>(p, E, H, gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs, st);
 }
 template <int R, bool OBS>
-void launch_march(const gca_alex_params& p, int E, int H, const uint8_t* gi, uint8_t* go, const int16_t* ai,
+void launch_march(const gca_alex_params& p, int E, int H, int W, const uint8_t* gi, uint8_t* go, const int16_t* ai,
                   int16_t* ao, const uint8_t* vd, const uint16_t* db, const float* es, const int32_t* wi,
                   const uint32_t* rs, int32_t* counts, const uint8_t* act_in, uint8_t* act_out, MarchObs obs,
                   hipStream_t st) {
     if (p.p_tree > 0.0f)
-        launch_march_g<R, OBS, true>(p, E, H, gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs, st);
+        launch_march_g<R, OBS, true>(p, E, H, W, gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs, st);
     else
-        launch_march_g<R, OBS, false>(p, E, H, gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs, st);
+        launch_march_g<R, OBS, false>(p, E, H, W, gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs, st);
 }
 
 template <bool OBS>
-void dispatch_march(const gca_alex_params& p, int E, int H, const uint8_t* gi, uint8_t* go, const int16_t* ai,
+void dispatch_march(const gca_alex_params& p, int E, int H, int W, const uint8_t* gi, uint8_t* go, const int16_t* ai,
                     int16_t* ao, const uint8_t* vd, const uint16_t* db, const float* es, const int32_t* wi,
                     const uint32_t* rs, int32_t* counts, const uint8_t* act_in, uint8_t* act_out, MarchObs obs,
                     hipStream_t st) {
 #define GCA_MARCH_CASE(RV) \
-    case RV: launch_march<RV, OBS>(p, E, H, gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs, st); break;
+    case RV: launch_march<RV, OBS>(p, E, H, W, gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs, st); break;
     switch (p.R) {
         GCA_MARCH_CASE(1) GCA_MARCH_CASE(2) GCA_MARCH_CASE(3) GCA_MARCH_CASE(4)
         GCA_MARCH_CASE(5) GCA_MARCH_CASE(6) GCA_MARCH_CASE(7) GCA_MARCH_CASE(8)
@@ -709,10 +847,13 @@ int march_impl(const gca_alex_params* p, int E, int H, int W, const uint8_t* gri
                const uint8_t* act_in, uint8_t* act_out, MarchObs obs, void* stream) {
     GCA_CHECK_ARG(p && grid_in && grid_out && age_in && age_out && vd && dous_bits && edge_slope && wind_index,
                   "alex_step_march: null argument");
-    GCA_CHECK_ARG(E > 0 && H > 0 && W == MW && H % SH == 0, "alex_step_march: W must be 256 and H a multiple of 16");
+    GCA_CHECK_ARG(E > 0 && H > 0 && (W == MW || W == 2 * MW || W == 4 * MW) && H % SH == 0,
+                  "alex_step_march: W must be 256, 512 or 1024 and H a multiple of 16");
     GCA_CHECK_ARG(p->R >= 1 && p->R <= GCA_MAX_RADIUS, "alex_step_march: burn radius must be in [1, 8]");
     GCA_CHECK_ARG(p->n_winds >= 1 && p->n_winds <= 16, "alex_step_march: 1..16 wind matrices");
-    GCA_CHECK_ARG((int64_t)E * (H / SH) < (int64_t)1 << 31, "alex_step_march: too many tiles");
+    GCA_CHECK_ARG((int64_t)E * (H / SH) * (W / MW) < (int64_t)1 << 31, "alex_step_march: too many tiles");
+    GCA_CHECK_ARG(!act_in || W == MW, "alex_step_march: the tile activity map (act_in) is read at W = 256 only (wider "
+                                      "grids find quiet strips from the grid itself; act_out is still written)");
     GCA_CHECK_ARG(grid_in != grid_out, "alex_step_march: the grid cannot be updated in place");
     GCA_CHECK_ARG(((((uintptr_t)grid_in) | ((uintptr_t)grid_out) | ((uintptr_t)age_in) | ((uintptr_t)age_out) |
                     ((uintptr_t)vd) | ((uintptr_t)edge_slope) | ((uintptr_t)obs.rgb) | ((uintptr_t)obs.col)) & 15u) == 0 &&
@@ -727,10 +868,10 @@ int march_impl(const gca_alex_params* p, int E, int H, int W, const uint8_t* gri
     }
     const uint8_t* ain = (p->p_tree > 0.0f) ? nullptr : act_in;  // growth can change a fire-free tile
     if (obs.rgb)
-        dispatch_march<true>(*p, E, H, grid_in, grid_out, age_in, age_out, vd, dous_bits, edge_slope, wind_index,
+        dispatch_march<true>(*p, E, H, W, grid_in, grid_out, age_in, age_out, vd, dous_bits, edge_slope, wind_index,
                              rng_step, counts, ain, act_out, obs, st);
     else
-        dispatch_march<false>(*p, E, H, grid_in, grid_out, age_in, age_out, vd, dous_bits, edge_slope, wind_index,
+        dispatch_march<false>(*p, E, H, W, grid_in, grid_out, age_in, age_out, vd, dous_bits, edge_slope, wind_index,
                               rng_step, counts, ain, act_out, obs, st);
     GCA_CHECK_LAUNCH(obs.rgb ? "alex_step_march_rgb" : "alex_step_march");
     return GCA_OK;

@@ -116,8 +116,8 @@ class AdvancedForestFireBulldozerEnv:
         self.slope_layout = slope_layout
         if step_kernel not in ("auto", "march", "tiled"):
             raise ValueError("step_kernel must be 'auto', 'march' or 'tiled'")
-        if step_kernel == "march" and (slope_layout != "packed" or W != 256):
-            raise ValueError("step_kernel='march' needs the packed layout at W = 256")
+        if step_kernel == "march" and (slope_layout != "packed" or W not in (256, 512, 1024)):
+            raise ValueError("step_kernel='march' needs the packed layout at W = 256, 512 or 1024")
         self._step_kernel = step_kernel
         if slope_layout == "packed":  # the packed step updates ages in place: both "buffers" are one (stride 0)
             self.age = torch.zeros((E, H, W), dtype=torch.int16, **kw).unsqueeze(0).expand(2, E, H, W)
@@ -233,8 +233,9 @@ class AdvancedForestFireBulldozerEnv:
 
     @property
     def march(self):
-        """True when the packed step runs the marching kernel (W = 256; edge slopes in natural column order)."""
-        return self.slope_layout == "packed" and self.ncols == 256 and self._step_kernel != "tiled"
+        """True when the packed step runs the marching kernel (W = 256, 512, 1024; edge slopes in natural column
+        order); other widths (W % 256 == 0) run the tiled kernel on the coalesced layout."""
+        return self.slope_layout == "packed" and self.ncols in (256, 512, 1024) and self._step_kernel != "tiled"
 
     def _slopes_from(self, altitude):
         E, H, W = self.num_envs, self.nrows, self.ncols

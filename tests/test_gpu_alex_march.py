@@ -77,10 +77,11 @@ def _with_radius(p, R):
 
 
 @pytest.mark.parametrize("R", [1, 2, 3, 4, 5, 6, 7, 8])
-@pytest.mark.parametrize("E,H,seed,p_tree", [(2, 256, 41, 0.0), (3, 48, 42, 0.01), (2, 16, 43, 0.0)])
-def test_march_matches_packed(device, R, E, H, seed, p_tree):
-    """Grid, ages, counts and the activity map out of the marching step equal the tiled step's, three steps on."""
-    W = 256
+@pytest.mark.parametrize("E,H,W,seed,p_tree", [(2, 256, 256, 41, 0.0), (3, 48, 256, 42, 0.01), (2, 16, 256, 43, 0.0),
+                                               (2, 64, 512, 44, 0.0), (3, 32, 512, 45, 0.01), (1, 48, 1024, 46, 0.0)])
+def test_march_matches_packed(device, R, E, H, W, seed, p_tree):
+    """Grid, ages, counts and the activity map out of the marching step equal the tiled step's, three steps on; at W =
+    512 / 1024 the segment waves of a strip exchange their edge values (every radius crosses the boundaries)."""
     case = make_case(E, H, W, seed, p_tree=p_tree, dousing_p=0.2, fire_p=0.05)
     p = _with_radius(params(H, p_tree, seed=seed * 5), R)
     es, _ = slopes(device, altitude(E, H, W, seed))
@@ -161,10 +162,17 @@ def test_march_rejects_bad_shapes(device):
     from gymca_amd._lib import GCAError, call
 
     p = params(16)
+    for W in (384, 768, 2048):  # widths the kernel does not take (256, 512, 1024 only)
+        g = torch.zeros((1, 16, W), dtype=torch.uint8, device=device)
+        with pytest.raises(GCAError):
+            call("gca_alex_step_march", p, 1, 16, W, dev.ptr(g), dev.ptr(g.clone()), dev.ptr(g), dev.ptr(g),
+                 dev.ptr(g), dev.ptr(g), dev.ptr(g), dev.ptr(g), None, None, None, None, dev.stream_ptr())
+    # the tile activity map is read at W = 256 only
     g = torch.zeros((1, 16, 512), dtype=torch.uint8, device=device)
+    act = torch.ones((2, 2), dtype=torch.uint8, device=device)
     with pytest.raises(GCAError):
         call("gca_alex_step_march", p, 1, 16, 512, dev.ptr(g), dev.ptr(g.clone()), dev.ptr(g), dev.ptr(g), dev.ptr(g),
-             dev.ptr(g), dev.ptr(g), dev.ptr(g), None, None, None, None, dev.stream_ptr())
+             dev.ptr(g), dev.ptr(g), dev.ptr(g), None, None, dev.ptr(act[0]), dev.ptr(act[1]), dev.stream_ptr())
 
 
 def test_march_other_cell_codes(device):
@@ -216,3 +224,71 @@ def test_march_quiet_tiles_from_the_grid(device):
         assert np.array_equal(a1, a0) and np.array_equal(c1, c0) and np.array_equal(t1, t0), f"step {s}"
         case["grid"], case["age"] = g1, a1
     assert (case["grid"][1] != 2).all()
+
+
+@pytest.mark.parametrize("W", [512, 1024])
+def test_march_segment_boundaries(device, W):
+    """Fires, dousing and steep slopes placed on and next to the segment boundaries (columns 255 | 256, 511 | 512, ...)
+    and the grid's side borders, growth on: the marching step at W = 512 / 1024 equals the tiled step and the C oracle
+    (grid, ages, counts, map) over three steps, and its fused frame equals the tiled kernel's (night and day)."""
+    import torch
+
+    from gymca_amd import _device as dev
+    from gymca_amd._lib import call
+    from gymca_amd.forest_fire.bulldozer.observation import make_obs_params
+
+    E, H = 2, 48
+    case = make_case(E, H, W, 81 + W, p_tree=0.02, dousing_p=0.0, fire_p=0.0)
+    for b in range(0, W + 1, 256):  # every segment edge and the two borders
+        for c in (b - 2, b - 1, b, b + 1):
+            if 0 <= c < W:
+                case["grid"][0, 3:45:3, c] = 2
+                case["grid"][1, 20:24, c] = 2
+                case["dous"][0, 10:40:4, c] = 1
+    case["age"][case["grid"] == 2] = 5
+    p = _with_radius(params(H, 0.02, seed=13), 8 if W == 1024 else 7)
+    es, ps = slopes(device, altitude(E, H, W, 17) * 3.0)  # steep: large slope factors either way
+    coal = _coalesced(device, es)
+    vd, bits = _layers(device, case)
+    for s in range(3):
+        rs = np.full(E, 5 + s, np.uint32)
+        g0, a0, c0, t0, _ = _run(device, "gca_alex_step_packed", p, case, coal, rs, vd, bits)
+        g1, a1, c1, t1, _ = _run(device, "gca_alex_step_march", p, case, es, rs, vd, bits)
+        go, ao, co, _ = alex_c.alex_step(p, case["grid"], case["age"], case["veg"], case["den"], case["dous"],
+                                         ps.cpu().numpy(), case["widx"], rng_step=rs)
+        assert np.array_equal(g1, g0), f"step {s}: {np.argwhere(g1 != g0)[:5]}"
+        assert np.array_equal(g1, go) and np.array_equal(a1, ao) and np.array_equal(c1, co)
+        assert np.array_equal(a1, a0) and np.array_equal(c1, c0) and np.array_equal(t1, t0)
+        case["grid"], case["age"] = g1, a1
+    op = make_obs_params(0, 1, 2, False, False, 8)
+    col = torch.zeros((12, 4), dtype=torch.float32, device=device)
+    call("gca_obs_color_table", op, dev.ptr(col), dev.stream_ptr())
+    night = torch.as_tensor(np.array([0, 1], np.int32), device=device)
+    rs = np.full(E, 9, np.uint32)
+    ref = _run(device, "gca_alex_step_packed_rgb", p, case, coal, rs, vd, bits, rgb=(col, night))
+    got = _run(device, "gca_alex_step_march_rgb", p, case, es, rs, vd, bits, rgb=(col, night))
+    for k in range(5):
+        assert np.array_equal(got[k], ref[k]), k
+
+
+def test_march_wide_quiet_strips(device):
+    """W = 512 without a map: a strip is copied only when no segment of it holds a FIRE near it (one consensus per
+    workgroup); a FIRE in the right segment's first column next to a TREE in the left segment's last column must
+    still burn across the boundary. Equal to the tiled kernel over three steps."""
+    E, H, W = 2, 64, 512
+    case = make_case(E, H, W, 91, p_tree=0.0, dousing_p=0.1, fire_p=0.0)
+    case["grid"][0, 20, 256] = 2  # right segment only; the left segment's column 255 trees sit next to it
+    case["grid"][0, 20, 255] = 1
+    case["grid"][1, 47, 511] = 2  # last column, last row of a strip
+    case["age"][case["grid"] == 2] = 9
+    p = params(H, 0.0, seed=3)
+    es, _ = slopes(device, altitude(E, H, W, 91))
+    coal = _coalesced(device, es)
+    vd, bits = _layers(device, case)
+    for s in range(3):
+        rs = np.full(E, s, np.uint32)
+        g0, a0, c0, t0, _ = _run(device, "gca_alex_step_packed", p, case, coal, rs, vd, bits)
+        g1, a1, c1, t1, _ = _run(device, "gca_alex_step_march", p, case, es, rs, vd, bits)
+        assert np.array_equal(g1, g0) and np.array_equal(a1, a0) and np.array_equal(c1, c0)
+        assert np.array_equal(t1, t0)
+        case["grid"], case["age"] = g1, a1

@@ -158,8 +158,8 @@ def test_headline_sizes_injected_vs_reference_rule(device, N, seed):
     1. gca_alex_step (8 p_slope planes) and gca_alex_step_es (edge slopes) vs the numpy restatement of
        _update_grid (ca_alexandridis_jax.py:62,108-153,345-349,379-398) and the float64 probability;
     2. the two layouts bit-identical (states, ages, counts, probabilities);
-    3. the headline kernels, gca_alex_step_packed (tiled) and at W = 256 gca_alex_step_march (the env's step
-       there; Philox mode, packed layout), bit-identical to gca_alex_step_es in Philox mode on the same state,
+    3. the headline kernels, gca_alex_step_packed (tiled) and gca_alex_step_march (the env's step at W = 256 and
+       512; Philox mode, packed layout), bit-identical to gca_alex_step_es in Philox mode on the same state,
        whose probabilities are bit-identical to the injected-mode probabilities checked in 1 — so the timed
        kernel evaluates the reference's p_d."""
     import torch
@@ -199,7 +199,7 @@ def test_headline_sizes_injected_vs_reference_rule(device, N, seed):
     g_es, a_es, c_es, po_es = step(device, "gca_alex_step_es", p, case_ph, es, rng_step=rs, probs=True)
     g_pk, a_pk, c_pk, _, _ = packed_step(device, p, case_ph, es, rs)
     assert np.array_equal(g_pk, g_es) and np.array_equal(a_pk, a_es) and np.array_equal(c_pk, c_es)
-    if N == 256:
+    if N in (256, 512):  # the env's step at both sizes (W = 512: two segment waves per strip, R = 7)
         from test_gpu_alex_march import _layers, _run
 
         vd, bits = _layers(device, case_ph)
