@@ -7,9 +7,11 @@ R=$(pwd)
 V=$R/gym-cellular-automata_amd/gymca_amd/_lib/variants
 O=gpurun_out/$TAG
 mkdir -p $O
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest_gpu.log 2>&1
-echo "pytest exit $?" >> $O/pytest_gpu.log
-grep -q "pytest exit 0" $O/pytest_gpu.log || exit 20
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest_gpu.log 2>&1
+RC=$?
+echo "pytest exit $RC" >> $O/pytest_gpu.log
+# 1 = some test failed (read the log, go on measuring); anything else (crash, abort, time limit): stop here
+[ $RC -eq 0 ] || [ $RC -eq 1 ] || exit 20
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 21
 timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err || exit 22
 for pass in 1 2; do
