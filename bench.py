@@ -169,6 +169,25 @@ def synthetic_state(env, rank, device):
     env.set_state(grid=grid, fire_age=age, wind_index=widx)
 
 
+def env_snapshot(env, step_fn, n_steps):
+    """A `prepare` for timed_loop: the env's state after reset + `n_steps` untimed steps of `step_fn` (every env well
+    into its episode, the RepeatCA accumulators spread out as in a long run), saved once (a copy of every tensor
+    attribute of the env) and restored in place before each loop / repetition, so every figure of a section times the
+    same steps from the same mid-episode state."""
+    import torch
+
+    env.reset()
+    for _ in range(n_steps):
+        step_fn()
+    saved = {k: v.clone() for k, v in vars(env).items() if isinstance(v, torch.Tensor)}
+
+    def restore():
+        for k, v in saved.items():
+            getattr(env, k).copy_(v)
+
+    return restore
+
+
 def timed_loop(step_fn, K, W, pg, device, reps=1, detail=None, prepare=None):
     """W untimed steps, then `reps` repetitions of EXACTLY K steps, each bracketed by barrier + synchronize on
     both sides, max over ranks. Returns (median seconds per K steps, mean kernel seconds from the events
@@ -425,14 +444,15 @@ def bench_windy(args, world, rank, device, pg):
         env.step(action)
 
     K = max(args.steps, 40)
-    # every loop starts from the same reset state (env.reset: the seeded initial distribution, RNG counters at 0), so
-    # the eager and graph figures time the same stretch of the same trajectories
+    # every loop starts from the same mid-episode state (reset + 64 steps, restored in place), so the eager and graph
+    # figures time the same stretch of the same trajectories
     G = 8
     Kg = max(K // G, 5)
-    dt_eager, _ = timed_loop(lambda ev: one_step(), Kg * G, args.warmup, pg, device, reps=3, prepare=env.reset)
+    restore = env_snapshot(env, one_step, 64)
+    dt_eager, _ = timed_loop(lambda ev: one_step(), Kg * G, 0, pg, device, reps=3, prepare=restore)
     # the same steps replayed from one HIP graph per G env steps (no host launch overhead)
     graph = StepGraph(one_step, n_steps=G, device=device)
-    dt_env, _ = timed_loop(lambda ev: graph.replay(), Kg, 2, pg, device, reps=3, prepare=env.reset)
+    dt_env, _ = timed_loop(lambda ev: graph.replay(), Kg, 0, pg, device, reps=3, prepare=restore)
     # CA-only (steps[E] = 1 forced), dense variant {0:.1, 3:.6, 25:.3}
     g = env.grids()
     u = torch.rand(g.shape, device=device)
@@ -472,7 +492,8 @@ def bench_windy(args, world, rank, device, pg):
         "config": "ForestFireBulldozer 256x256, 1024 envs/GPU, WindyForestFire",
         "env_steps_per_s": world * E * Kg * G / dt_env,
         "env_steps_per_s_eager": world * E * Kg * G / dt_eager,
-        "loops": f"eager and graph: {Kg * G} env steps from the same reset state, median of 3",
+        "loops": f"eager and graph: the same {Kg * G} env steps from one mid-episode state (reset + 64 steps, restored "
+                 f"before each repetition), median of 3",
         "env_step_graph": f"hipGraph of {G} env steps (random actions + " + (
             "gca_bulldozer_step_fused: RepeatCA, Windy CA, Move/Modify and reward in one launch)" if env.fused else
             "RepeatCA/Windy passes + Move/Modify + reward)"),
@@ -528,15 +549,16 @@ def bench_windy512(args, world, rank, device, pg):
         one_step()
         gather(async_op=True)
 
-    dt_eager, _ = timed_loop(eager, K, args.warmup, pg, device, reps=3, prepare=env.reset)
-    dt_async, _ = timed_loop(overlapped, K, args.warmup, pg, device, reps=3, prepare=env.reset)
+    restore = env_snapshot(env, one_step, 64)
+    dt_eager, _ = timed_loop(eager, K, 0, pg, device, reps=3, prepare=restore)
+    dt_async, _ = timed_loop(overlapped, K, 0, pg, device, reps=3, prepare=restore)
     graph = StepGraph(one_step, n_steps=G, device=device)
 
     def seg(ev):
         graph.replay()
         gather()
 
-    dt_g, _ = timed_loop(seg, Kg, 2, pg, device, reps=3, prepare=env.reset)
+    dt_g, _ = timed_loop(seg, Kg, 0, pg, device, reps=3, prepare=restore)
     # CA-only at HBM scale: one forced Windy step of every env, 268 MB per buffer (beyond the 256 MB
     # Infinity Cache, unlike config 2's 64 MiB pair), dense {0:.1, 3:.6, 25:.3}, beside a same-size copy
     ca = windy_ca_only(env, K, args.warmup, pg, device)
@@ -546,7 +568,8 @@ def bench_windy512(args, world, rank, device, pg):
                          "pre / Windy passes / post kernels"),
             "env_steps_per_s_eager_gather_every_step": world * E * K / dt_eager,
             "env_steps_per_s_async_gather_every_step": world * E * K / dt_async,
-            "loops": f"graph / eager / async: {K} env steps each from the same reset state, median of 3",
+            "loops": f"graph / eager / async: the same {K} env steps from one mid-episode state (reset + 64 steps, "
+                     f"restored before each repetition), median of 3",
             "gather": ("RCCL all_gather_into_tensor of reward f32 | length | done u8 per env into a reused buffer "
                        f"(gymca_amd.distributed.StatsGather: 1 pack + 1 collective), world {world}")
                       if world > 1 else "none (1 GPU)",

@@ -406,6 +406,33 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
     const uint32_t step = rng_step ? rng_step[e] : 0u;
     const uint32_t k0 = (uint32_t)p.seed, k1 = (uint32_t)(p.seed >> 32);
     const uint32_t env_id = (uint32_t)(p.env_offset + e);
+    // Philox4x32-10 of the counter (cell pair, env, step, tag) (gca_common.h philox4x32_10, bit for bit): words 1..3
+    // are the same for every block of the wave, so the first round's M1 x step product (words 0 / 1 after round 1)
+    // and the second round's M0 product of word 0 are wave constants, computed once here on the scalar unit; per block
+    // the lane does one multiply in each of the first two rounds instead of two (r04)
+    constexpr uint32_t PM0 = 0xD2511F53u, PM1 = 0xCD9E8D57u, PW0 = 0x9E3779B9u, PW1 = 0xBB67AE85u;
+    const uint64_t pq1 = (uint64_t)PM1 * step;
+    const uint32_t pu0 = (uint32_t)(pq1 >> 32) ^ env_id ^ k0;  // word 0 after round 1 (uniform)
+    const uint64_t pq2 = (uint64_t)PM0 * pu0;                   // round 2's word-0 product (uniform)
+    const uint32_t pkc = (uint32_t)GCA_TAG_ALEX_CELL ^ k1;      // round 1: word 2 = hi0 ^ tag ^ k1
+    const uint32_t pka = (uint32_t)pq1 ^ (k0 + PW0);            // round 2: word 0 = hi1 ^ (word 1 = lo(M1 step)) ^ key
+    const uint32_t pkb = (uint32_t)(pq2 >> 32) ^ (k1 + PW1);    // round 2: word 2 = hi(M0 pu0) ^ (word 3 = lo0) ^ key
+    const uint32_t pl2 = (uint32_t)pq2;                         // round 2: word 3 = lo(M0 pu0)
+    auto philox_cell = [&](uint32_t x0, uint32_t rk0, uint32_t rk1) -> u32x4 {
+        const uint64_t p0 = (uint64_t)PM0 * x0;  // round 1
+        const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        const uint64_t p1 = (uint64_t)PM1 * (hi0 ^ pkc);  // round 2 (word 2 after round 1)
+        u32x4 c = u32x4{(uint32_t)(p1 >> 32) ^ pka, (uint32_t)p1, lo0 ^ pkb, pl2};
+#pragma unroll
+        for (int i = 2; i < 10; ++i) {  // rounds 3..10 as philox4x32_10, keys (k0 + i W0, k1 + i W1)
+            const uint64_t a = (uint64_t)PM0 * c.x;
+            const uint64_t b = (uint64_t)PM1 * c.z;
+            const uint32_t n0 = __builtin_amdgcn_bitop3_b32((uint32_t)(b >> 32), c.y, rk0 + (uint32_t)i * PW0, 0x96);
+            const uint32_t n2 = __builtin_amdgcn_bitop3_b32((uint32_t)(a >> 32), c.w, rk1 + (uint32_t)i * PW1, 0x96);
+            c = u32x4{n0, (uint32_t)b, n2, (uint32_t)a};
+        }
+        return c;
+    };
     const float pt24 = __fmul_rn(p.p_tree, 16777216.0f);
     const float w_in_minus_bd = __fsub_rn(p.dous_inner, p.dous_border);
     const uint32_t codes = (p.empty & 0xFFu) | ((p.tree & 0xFFu) << 8) | ((p.fire & 0xFFu) << 16);
@@ -707,7 +734,7 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
         for (int h = 0; h < 2; ++h) {
             u32x4 X = u32x4{0u, 0u, 0u, 0u};
             if (wave_draws)
-                X = philox4x32_10(u32x4{(lin0 >> 1) + (uint32_t)h, env_id, step, GCA_TAG_ALEX_CELL}, rk0, rk1);
+                X = philox_cell((lin0 >> 1) + (uint32_t)h, rk0, rk1);
             // thr = fl(1 - qn) * 2^24 = fl(2^24 - qn * 2^24) (power-of-two scaling commutes with the rounding)
             const gca_f2 thr = __builtin_elementwise_fma(qn[h], (gca_f2){-16777216.0f, -16777216.0f},
                                                          (gca_f2){16777216.0f, 16777216.0f});

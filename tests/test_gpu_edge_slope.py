@@ -290,17 +290,19 @@ def test_env_packed_and_edge_layouts_agree(device):
 
 @pytest.mark.parametrize("pinecones", [False, True])
 def test_tile_skip_matches_full_step(device, pinecones):
-    """The packed step's tile activity map (tiles with no fire in their 3 x 3 tile neighbourhood are copied,
+    """The tiled packed step's tile activity map (tiles with no fire in their 3 x 3 tile neighbourhood are copied,
     not stepped) changes nothing: env trajectories from the reset state (two fires per env: most tiles skip)
-    and from a mid-episode state equal the same env with tile_skip=False, grid, ages, rewards and done, over
-    steps with shooting, pinecones (which ignite tiles far from the fire front) and a conditional reset."""
+    and from a mid-episode state equal the default env's (the marching step, which finds quiet tiles from the grid
+    itself and keeps no map even with tile_skip=True), grid, ages, rewards and done, over steps with shooting,
+    pinecones (which ignite tiles far from the fire front) and a conditional reset."""
     from gymca_amd.forest_fire.bulldozer import AdvancedForestFireBulldozerEnv
 
     E, N = 3, 256
     envs = [AdvancedForestFireBulldozerEnv(N, N, key=21, num_envs=E, use_hidden=True, device=device,
-                                           hidden_rng=np.random.RandomState(4), pinecones=pinecones, tile_skip=ts)
-            for ts in (True, False)]
-    assert envs[0].act is not None and envs[1].act is None
+                                           hidden_rng=np.random.RandomState(4), pinecones=pinecones, tile_skip=ts,
+                                           step_kernel=sk)
+            for ts, sk in ((True, "tiled"), (True, "auto"))]
+    assert envs[0].act is not None and not envs[0].march and envs[1].act is None and envs[1].march
     rng = np.random.default_rng(3)
     for phase in range(2):
         for env in envs:

@@ -106,12 +106,12 @@ def test_env_rgb_observation(device):
             assert np.array_equal(rgb[e].cpu().numpy(), want), (s, e)
 
 
-@pytest.mark.parametrize("W", [512, 256])
+@pytest.mark.parametrize("W", [768, 512, 256])
 @pytest.mark.parametrize("tile_skip", [False, True])
 def test_fused_step_observation_matches_reference(device, tile_skip, W):
     """The plain observation (enable_extensions=False, the reference's default) written by the CA step's own
-    epilogue on the packed layout (W = 512: gca_alex_step_packed_rgb, two tiles per row; W = 256: the marching
-    gca_alex_step_march_rgb) + the bulldozer's pixel (gca_obs_position) equals the literal restatement of
+    epilogue on the packed layout (W = 768: gca_alex_step_packed_rgb, the tiled step, three tiles per row; W = 256 /
+    512: the marching gca_alex_step_march_rgb, one / two segment waves per strip) + the bulldozer's pixel (gca_obs_position) equals the literal restatement of
     grid_to_rgb (advanced_bulldozer.py:1035-1101) of the post-step grid and position with the PRE-step dousing and
     day / night: over steps with shooting, a day / night toggle, the tile-skip path and a conditional reset."""
     import torch
@@ -121,7 +121,7 @@ def test_fused_step_observation_matches_reference(device, tile_skip, W):
     E, H = 3, 256
     env = AdvancedForestFireBulldozerEnv(H, W, key=8, num_envs=E, use_hidden=True, device=device, observation="grid",
                                          hidden_rng="philox", tile_skip=tile_skip)
-    assert env.march == (W == 256)
+    assert env.march == (W != 768)
     env.reset()
     # observation="rgb" needs a square grid for the reset frame; the step frame does not: give this env an RGB buffer
     env.rgb = torch.zeros((E, H, W, 3), dtype=torch.float32, device=device)
