@@ -118,6 +118,54 @@ __device__ __forceinline__ void window4(uint32_t X, int k, uint32_t (&B)[4], uin
 }
 
 __device__ __forceinline__ float4 ldf4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+// gca_edge_factors_both / _own (gca_alex_rule.h) with the first Newton fma as a builtin (v_pk_fma_f32 with the neg
+// modifier, the same instruction) instead of inline asm with its own s_nop: the hazard recogniser then spaces the
+// v_rcp_f32 -> v_pk_fma_f32 reads only where the schedule leaves them adjacent
+__device__ __forceinline__ gca_f2 m_recip(float v0, float v1) {
+    const gca_f2 x = {v0, v1};
+    const gca_f2 r0 = {__builtin_amdgcn_rcpf(v0), __builtin_amdgcn_rcpf(v1)};
+    const gca_f2 ee = __builtin_elementwise_fma(-x, r0, (gca_f2){1.0f, 1.0f});
+    return __builtin_elementwise_fma(ee, r0, r0);
+}
+__device__ __forceinline__ void m_edge_both(float v0, float v1, gca_f2& own, gca_f2& nb) {
+    const gca_f2 rc = m_recip(v0, v1);
+    asm("v_max_f32_e64 %0, %1, -%2" : "=v"(own.x) : "v"(v0), "v"(rc.x));
+    asm("v_max_f32_e64 %0, %1, -%2" : "=v"(own.y) : "v"(v1), "v"(rc.y));
+    asm("v_max_f32_e64 %0, -%1, %2" : "=v"(nb.x) : "v"(v0), "v"(rc.x));
+    asm("v_max_f32_e64 %0, -%1, %2" : "=v"(nb.y) : "v"(v1), "v"(rc.y));
+}
+// both cell pairs of a float4 at once: the two reciprocal chains interleaved (each v_pk_fma_f32 result is read two
+// instructions later, not by the next one)
+__device__ __forceinline__ void m_edge_both4(const float4& v, gca_f2& oa, gca_f2& na, gca_f2& ob, gca_f2& nb) {
+    const gca_f2 x0 = {v.x, v.y}, x1 = {v.z, v.w};
+    const gca_f2 r0 = {__builtin_amdgcn_rcpf(v.x), __builtin_amdgcn_rcpf(v.y)};
+    const gca_f2 r1 = {__builtin_amdgcn_rcpf(v.z), __builtin_amdgcn_rcpf(v.w)};
+    const gca_f2 e0 = __builtin_elementwise_fma(-x0, r0, (gca_f2){1.0f, 1.0f});
+    const gca_f2 e1 = __builtin_elementwise_fma(-x1, r1, (gca_f2){1.0f, 1.0f});
+    const gca_f2 c0 = __builtin_elementwise_fma(e0, r0, r0);
+    const gca_f2 c1 = __builtin_elementwise_fma(e1, r1, r1);
+    asm("v_max_f32_e64 %0, %1, -%2" : "=v"(oa.x) : "v"(v.x), "v"(c0.x));
+    asm("v_max_f32_e64 %0, %1, -%2" : "=v"(oa.y) : "v"(v.y), "v"(c0.y));
+    asm("v_max_f32_e64 %0, %1, -%2" : "=v"(ob.x) : "v"(v.z), "v"(c1.x));
+    asm("v_max_f32_e64 %0, %1, -%2" : "=v"(ob.y) : "v"(v.w), "v"(c1.y));
+    asm("v_max_f32_e64 %0, -%1, %2" : "=v"(na.x) : "v"(v.x), "v"(c0.x));
+    asm("v_max_f32_e64 %0, -%1, %2" : "=v"(na.y) : "v"(v.y), "v"(c0.y));
+    asm("v_max_f32_e64 %0, -%1, %2" : "=v"(nb.x) : "v"(v.z), "v"(c1.x));
+    asm("v_max_f32_e64 %0, -%1, %2" : "=v"(nb.y) : "v"(v.w), "v"(c1.y));
+}
+__device__ __forceinline__ void m_edge_own4(const float4& v, gca_f2& oa, gca_f2& ob) {
+    const gca_f2 x0 = {v.x, v.y}, x1 = {v.z, v.w};
+    const gca_f2 r0 = {__builtin_amdgcn_rcpf(v.x), __builtin_amdgcn_rcpf(v.y)};
+    const gca_f2 r1 = {__builtin_amdgcn_rcpf(v.z), __builtin_amdgcn_rcpf(v.w)};
+    const gca_f2 e0 = __builtin_elementwise_fma(-x0, r0, (gca_f2){1.0f, 1.0f});
+    const gca_f2 e1 = __builtin_elementwise_fma(-x1, r1, (gca_f2){1.0f, 1.0f});
+    const gca_f2 c0 = __builtin_elementwise_fma(e0, r0, r0);
+    const gca_f2 c1 = __builtin_elementwise_fma(e1, r1, r1);
+    asm("v_max_f32_e64 %0, %1, -%2" : "=v"(oa.x) : "v"(v.x), "v"(c0.x));
+    asm("v_max_f32_e64 %0, %1, -%2" : "=v"(oa.y) : "v"(v.y), "v"(c0.y));
+    asm("v_max_f32_e64 %0, %1, -%2" : "=v"(ob.x) : "v"(v.z), "v"(c1.x));
+    asm("v_max_f32_e64 %0, %1, -%2" : "=v"(ob.y) : "v"(v.w), "v"(c1.y));
+}
 // *(T*)((char*)base + off): a wave-uniform base and a 32-bit lane byte offset (global_load ... v_off, s[base])
 template <class T, class B> __device__ __forceinline__ T ld_at(const B* base, uint32_t off) {
     return *reinterpret_cast<const T*>(reinterpret_cast<const unsigned char*>(base) + off);
@@ -373,7 +421,8 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
     const uint32_t xo2 = HALO ? (lane == 63 ? (uint32_t)(((g + 2) * 4 + 1) * XI) : (uint32_t)((g * 4 + 2) * XI)) : 0u;
     // row s0's own factors of planes 0..2 (row r's directions 0..2 read prepared own factors; plane 3 stays raw)
     auto prep_own = [&](float4& v) {
-        const gca_f2 a = gca_edge_factors_own(v.x, v.y), b = gca_edge_factors_own(v.z, v.w);
+        gca_f2 a, b;
+        m_edge_own4(v, a, b);
         v = make_float4(col_lo ? 1.0f : a.x, a.y, b.x, col_hi ? 1.0f : b.y);
     };
 #pragma unroll
@@ -564,12 +613,10 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
         auto prep_next = [&](int k, bool want_nb, float (&nbv)[4]) {
             gca_f2 oa, ob, na, nb2;
             if (want_nb) {
-                gca_edge_factors_both(SN[k].x, SN[k].y, oa, na);
-                gca_edge_factors_both(SN[k].z, SN[k].w, ob, nb2);
+                m_edge_both4(SN[k], oa, na, ob, nb2);
                 nbv[0] = na.x; nbv[1] = na.y; nbv[2] = nb2.x; nbv[3] = nb2.y;
             } else {
-                oa = gca_edge_factors_own(SN[k].x, SN[k].y);
-                ob = gca_edge_factors_own(SN[k].z, SN[k].w);
+                m_edge_own4(SN[k], oa, ob);
             }
             SN[k] = make_float4(col_lo ? 1.0f : oa.x, oa.y, ob.x, col_hi ? 1.0f : ob.y);
         };
@@ -593,10 +640,12 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
                     else
                         window4(V[k], k, B, WZ);
                 }
+                gca_f2 bs[2];  // both pairs converted first, then both fmas (no dependent back-to-back packed op)
 #pragma unroll
                 for (int h = 0; h < 2; ++h)
-                    ph[h] = __builtin_elementwise_fma(bcast(hdwp[k >> 1], k & 1), k == 0 ? (gca_f2){(float)B[2 * h], (float)B[2 * h + 1]}
-                                                                       : wsum_f2(B[2 * h], B[2 * h + 1]), ph[h]);
+                    bs[h] = k == 0 ? (gca_f2){(float)B[2 * h], (float)B[2 * h + 1]} : wsum_f2(B[2 * h], B[2 * h + 1]);
+#pragma unroll
+                for (int h = 0; h < 2; ++h) ph[h] = __builtin_elementwise_fma(bcast(hdwp[k >> 1], k & 1), bs[h], ph[h]);
                 // one radius at a time (hipcc would otherwise interleave all the radii's DPP / dot4 work)
                 asm volatile("" : "+v"(ph[0]), "+v"(ph[1]));
                 __builtin_amdgcn_sched_barrier(0);
@@ -609,19 +658,33 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
                 window4(Dv1, 1, D1, WZ);
                 window4(Dv2, 2, D2, WZ);
             }
+            {  // the two pairs interleaved step by step (no packed result read by the next instruction)
+                gca_f2 d1[2], d2[2], dz[2];
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                gca_f2 dz = (gca_f2){w_in_minus_bd, w_in_minus_bd} * wsum_f2(D1[2 * h], D1[2 * h + 1]);
-                dz = __builtin_elementwise_fma((gca_f2){p.dous_border, p.dous_border}, wsum_f2(D2[2 * h], D2[2 * h + 1]), dz);
-                ph[h] = ph[h] - dz;
+                for (int h = 0; h < 2; ++h) d1[h] = wsum_f2(D1[2 * h], D1[2 * h + 1]);
+#pragma unroll
+                for (int h = 0; h < 2; ++h) d2[h] = wsum_f2(D2[2 * h], D2[2 * h + 1]);
+#pragma unroll
+                for (int h = 0; h < 2; ++h) dz[h] = (gca_f2){w_in_minus_bd, w_in_minus_bd} * d1[h];
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+                    dz[h] = __builtin_elementwise_fma((gca_f2){p.dous_border, p.dous_border}, d2[h], dz[h]);
+#pragma unroll
+                for (int h = 0; h < 2; ++h) ph[h] = ph[h] - dz[h];
             }
             // ---- base = (p_h * (1 + p_veg)) * (1 + p_den)
+            {
+                gca_f2 av[2], ad[2];
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const uint32_t b0 = (vdw >> (16 * h)) & 0xFFu, b1 = (vdw >> (16 * h + 8)) & 0xFFu;
-                const gca_f2 av = {lut[wl][b0 & 7u], lut[wl][b1 & 7u]};
-                const gca_f2 ad = {lut[wl][8 + (b0 >> 4)], lut[wl][8 + (b1 >> 4)]};
-                ph[h] = (ph[h] * av) * ad;
+                for (int h = 0; h < 2; ++h) {
+                    const uint32_t b0 = (vdw >> (16 * h)) & 0xFFu, b1 = (vdw >> (16 * h + 8)) & 0xFFu;
+                    av[h] = (gca_f2){lut[wl][b0 & 7u], lut[wl][b1 & 7u]};
+                    ad[h] = (gca_f2){lut[wl][8 + (b0 >> 4)], lut[wl][8 + (b1 >> 4)]};
+                }
+#pragma unroll
+                for (int h = 0; h < 2; ++h) ph[h] = ph[h] * av[h];
+#pragma unroll
+                for (int h = 0; h < 2; ++h) ph[h] = ph[h] * ad[h];
             }
             // ---- directions, in order: qn = prod over burning d of (1 - clamp01(base * wind[d] * p_slope[d])), each
             //      factor as qn = fma(-qn, c, qn);
@@ -634,17 +697,27 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
                     asm volatile("" : "+v"(ph[0]), "+v"(ph[1]), "+v"(qn[0]), "+v"(qn[1]));
                     const gca_f2 wd2 = bcast(windp[d >> 1], d & 1);
                     const uint32_t Md = dir_mask(d);
+                    // the two cell pairs' chains interleaved step by step (a packed f32 result read by the next
+                    // instruction costs a wait state; two independent chains hide it)
+                    gca_f2 t[2], c[2];
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) t[h] = ph[h] * wd2;
+#pragma unroll
+                    for (int h = 0; h < 2; ++h)
+                        c[h] = KILL ? (gca_f2){gca_clamp01(t[h].x), gca_clamp01(t[h].y)}
+                                    : gca_pk_mul_clamp01(t[h], (gca_f2){a[2 * h], a[2 * h + 1]});
+                    // qn <- fma(-qn, c, qn) = qn * (1 - c), one rounding (the oracle's order); no burning
+                    // neighbour d: c -> +0 and qn is unchanged exactly (the oracle skips the factor)
+                    uint32_t cm[2][2];
 #pragma unroll
                     for (int h = 0; h < 2; ++h) {
-                        const gca_f2 t = ph[h] * wd2;
-                        const gca_f2 c = KILL ? (gca_f2){gca_clamp01(t.x), gca_clamp01(t.y)}
-                                              : gca_pk_mul_clamp01(t, (gca_f2){a[2 * h], a[2 * h + 1]});
-                        // qn <- fma(-qn, c, qn) = qn * (1 - c), one rounding (the oracle's order); no burning
-                        // neighbour d: c -> +0 and qn is unchanged exactly (the oracle skips the factor)
-                        const uint32_t c0 = __float_as_uint(c.x) & (uint32_t)(int32_t)(int8_t)(Md >> (16 * h));
-                        const uint32_t c1 = __float_as_uint(c.y) & (uint32_t)(int32_t)(int8_t)(Md >> (16 * h + 8));
-                        qn[h] = __builtin_elementwise_fma(-qn[h], (gca_f2){__uint_as_float(c0), __uint_as_float(c1)}, qn[h]);
+                        cm[h][0] = __float_as_uint(c[h].x) & (uint32_t)(int32_t)(int8_t)(Md >> (16 * h));
+                        cm[h][1] = __float_as_uint(c[h].y) & (uint32_t)(int32_t)(int8_t)(Md >> (16 * h + 8));
                     }
+#pragma unroll
+                    for (int h = 0; h < 2; ++h)
+                        qn[h] = __builtin_elementwise_fma(-qn[h], (gca_f2){__uint_as_float(cm[h][0]), __uint_as_float(cm[h][1])},
+                                                          qn[h]);
                     __builtin_amdgcn_sched_barrier(0);
                 };
                 const float one[4] = {1.0f, 1.0f, 1.0f, 1.0f};
@@ -654,7 +727,7 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
                 uint32_t h45 = 0x3F800000u, h7 = 0x3F800000u;
                 if constexpr (HALO && !KILL) {
                     gca_f2 o_, n_;
-                    gca_edge_factors_both(__uint_as_float(xr[XS_ONE]), __uint_as_float(xr[XS_TWO]), o_, n_);
+                    m_edge_both(__uint_as_float(xr[XS_ONE]), __uint_as_float(xr[XS_TWO]), o_, n_);
                     h45 = __float_as_uint(n_.x);
                     h7 = __float_as_uint(n_.y);
                 }
@@ -668,8 +741,7 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
                     apply(4, one);
                 } else {  // plane 3 of row r: own factor (d = 3) and, one column on, the neighbour factor (d = 4)
                     gca_f2 oa, ob, na, nb2;
-                    gca_edge_factors_both(SC[3].x, SC[3].y, oa, na);
-                    gca_edge_factors_both(SC[3].z, SC[3].w, ob, nb2);
+                    m_edge_both4(SC[3], oa, na, ob, nb2);
                     const float a3[4] = {col_lo ? 1.0f : oa.x, oa.y, ob.x, col_hi ? 1.0f : ob.y};
                     apply(3, a3);
                     // (r, c+1)'s plane 3; lane 63's last cell is column 255 (DPP old = 1.0; HALO: the right segment's)
