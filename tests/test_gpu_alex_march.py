@@ -292,3 +292,37 @@ def test_march_wide_quiet_strips(device):
         assert np.array_equal(g1, g0) and np.array_equal(a1, a0) and np.array_equal(c1, c0)
         assert np.array_equal(t1, t0)
         case["grid"], case["age"] = g1, a1
+
+
+@pytest.mark.parametrize("N,pinecones", [(512, False), (512, True), (1024, False)])
+def test_env_march_equals_tiled_at_wide_grids(device, N, pinecones):
+    """The Advanced env at 512^2 / 1024^2 (R = 7 / 8, the reference's grid sizes above the headline) runs the marching
+    step (segment waves per strip); the same env on the tiled step (step_kernel="tiled") reproduces its trajectory
+    bit for bit: grids, ages, rewards, done, positions, over steps with shooting, pinecone spotting and a conditional
+    reset (advanced_bulldozer.py:332-518)."""
+    from gymca_amd.forest_fire.bulldozer import AdvancedForestFireBulldozerEnv
+
+    E = 2
+    envs = [AdvancedForestFireBulldozerEnv(N, N, key=31, num_envs=E, use_hidden=True, device=device,
+                                           hidden_rng="philox", observation="grid", pinecones=pinecones,
+                                           step_kernel=sk) for sk in ("auto", "tiled")]
+    assert envs[0].march and not envs[1].march
+    assert envs[0].alex_params.R == (7 if N == 512 else 8)
+    case = make_case(E, N, N, 33, fire_p=0.03, hidden=False)
+    for env in envs:
+        env.reset()
+        env.set_state(grid=case["grid"], fire_age=case["age"], wind_index=case["widx"])
+    rng = np.random.default_rng(5)
+    for t in range(6):
+        act = np.stack([rng.integers(0, 9, E), rng.integers(0, 2, E)], axis=1)
+        outs = [env.step(act) for env in envs]
+        a, b = envs
+        assert np.array_equal(a.grid[a.cur].cpu().numpy(), b.grid[b.cur].cpu().numpy()), t
+        assert np.array_equal(a.age[a.cur].cpu().numpy(), b.age[b.cur].cpu().numpy()), t
+        assert np.array_equal(outs[0][1].cpu().numpy(), outs[1][1].cpu().numpy())
+        assert np.array_equal(outs[0][2].cpu().numpy(), outs[1][2].cpu().numpy())
+        assert np.array_equal(a.pos.cpu().numpy(), b.pos.cpu().numpy())
+        if t == 3:
+            for env in envs:
+                env.done[0] = 1
+                env.conditional_reset()
