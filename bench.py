@@ -913,7 +913,7 @@ def headline_kernel_key(env):
     R = int(env.alex_params.R)
     grow = "true" if env.alex_params.p_tree > 0 else "false"
     if getattr(env, "march", False):
-        return f"alex_march<{R}, false, {grow}>"
+        return f"alex_march<{R}, false, {grow}, {int(env.ncols) // 256}>"
     es = "true" if env.slope_layout in ("packed", "edge") else "false"
     pk = "true" if env.slope_layout == "packed" else "false"
     return f"alex_step<{R}, 0, true, {es}, {pk}, false>"

@@ -27,10 +27,12 @@ def _tree(tmp_path):
 def test_headline_key_names_the_launched_template():
     bench = _bench()
     p = types.SimpleNamespace(R=6, p_tree=0.0)
-    env = types.SimpleNamespace(alex_params=p, march=True, slope_layout="packed")
-    assert bench.headline_kernel_key(env) == "alex_march<6, false, false>"
+    env = types.SimpleNamespace(alex_params=p, march=True, slope_layout="packed", ncols=256)
+    assert bench.headline_kernel_key(env) == "alex_march<6, false, false, 1>"
     p.p_tree = 0.5
-    assert bench.headline_kernel_key(env) == "alex_march<6, false, true>"
+    assert bench.headline_kernel_key(env) == "alex_march<6, false, true, 1>"
+    env.ncols = 512
+    assert bench.headline_kernel_key(env) == "alex_march<6, false, true, 2>"
     env = types.SimpleNamespace(alex_params=types.SimpleNamespace(R=7, p_tree=0.0), march=False, slope_layout="packed")
     assert bench.headline_kernel_key(env) == "alex_step<7, 0, true, true, true, false>"
     env.slope_layout = "planes"
@@ -41,9 +43,9 @@ def test_profile_entry_requires_the_same_sources(tmp_path, monkeypatch):
     bench = _bench()
     _tree(tmp_path)
     monkeypatch.setattr(bench, "ROOT", str(tmp_path))
-    key = "alex_march<6, false, false>"
+    key = "alex_march<6, false, false, 1>"
     sha = bench.kernel_src_sha(key)
-    assert sha and sha == bench.kernel_src_sha("alex_march<6, false, true>")  # one family, one source set
+    assert sha and sha == bench.kernel_src_sha("alex_march<6, false, true, 2>")  # one family, one source set
     args = types.SimpleNamespace(envs=4096, size=256)
     entry = {"bytes_per_launch": 7.0e9, "valu_busy": 0.9, "tag": "rX", "src_sha": sha}
     (tmp_path / "profiles" / "pmc_traffic.json").write_text(json.dumps({key: entry, "alex_march<6, false>": {
@@ -51,7 +53,7 @@ def test_profile_entry_requires_the_same_sources(tmp_path, monkeypatch):
     e, info = bench.profile_entry(args, key)
     assert e["bytes_per_launch"] == 7.0e9 and info["match"] and info["tag"] == "rX"
     # another template instance of the same family: no entry -> null, never a neighbour's figures
-    e, info = bench.profile_entry(args, "alex_march<6, true, false>")
+    e, info = bench.profile_entry(args, "alex_march<6, true, false, 1>")
     assert e is None and not info["match"]
     # an entry without a source stamp (older profile) -> null
     e, info = bench.profile_entry(args, "alex_march<6, false>")
