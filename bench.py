@@ -851,6 +851,43 @@ def bench_dropins(device):
     return out
 
 
+def bench_alex512(args, world, rank, device, pg):
+    """The Alexandridis step at the reference's next grid size, 512^2 (R = 7, ca_alexandridis_jax.py:62), 1024 envs
+    (the headline's 268M cells): the env's marching step (two segment waves per strip) against the tiled packed step on
+    the same C3-like state, mean launch time from HIP events (median of 3), no host work in the timed region."""
+    import torch
+
+    from gymca_amd.forest_fire.bulldozer import AdvancedForestFireBulldozerEnv
+
+    E, N = 1024, 512
+    env = AdvancedForestFireBulldozerEnv(N, N, key=1, num_envs=E, use_hidden=False, device=device, env_offset=rank * E,
+                                         observation="grid")
+    env.reset()
+    synthetic_state(env, rank, device)
+    times = []
+    for _ in range(3):
+        synthetic_state(env, rank, device)
+        env.ca_step()
+        torch.cuda.synchronize(device)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(10):
+            env.ca_step()
+        b.record()
+        torch.cuda.synchronize(device)
+        times.append(a.elapsed_time(b) / 10)
+    march_ms = sorted(times)[1]
+    tiled_ms = tiled_kernel_ms(env, device)
+    out = {"config": "AdvancedBulldozer 512x512 (R = 7), 1024 envs, use_hidden=False, C3-like mid-episode state",
+           "kernel": headline_kernel_key(env), "march_kernel_ms": march_ms, "tiled_kernel_ms": tiled_ms,
+           "march_over_tiled": march_ms / tiled_ms,
+           "cell_updates_per_s": E * N * N / (march_ms * 1e-3),
+           "moved_gbs": ALEX_BYTES["packed"] * E * N * N / (march_ms * 1e-3) / 1e9}
+    del env
+    torch.cuda.empty_cache()
+    return out
+
+
 def tiled_kernel_ms(env, device, K=10, reps=3):
     """The same C3 state through the tiled packed kernel (gca_alex_step_packed, coalesced slopes) that the marching
     kernel replaced at W = 256: mean launch time (HIP events, median of reps), for the record beside kernel_ms."""
@@ -990,6 +1027,7 @@ def main():
     gc.collect()
     torch.cuda.empty_cache()
     config4 = None if args.no_secondary else bench_config4(args, world, rank, device, pg)
+    alex512 = None if (args.no_secondary or args.size != 256) else bench_alex512(args, world, rank, device, pg)
     secondary = None if args.no_secondary else bench_windy(args, world, rank, device, pg)
     config5 = None if args.no_secondary else bench_windy512(args, world, rank, device, pg)
     dropins = None if (args.no_secondary or world > 1) else bench_dropins(device)
@@ -1062,6 +1100,7 @@ def main():
             "cpu_baseline": cpu,
             "secondary": secondary,
             "config4": config4,
+            "alex_512": alex512,
             "config5": config5,
             "dropins": dropins,
         }
