@@ -321,12 +321,18 @@ __device__ __forceinline__ RowCls<NW> classify_row(const RowRaw<NW>& x, bool val
 // the strip's new-grid counts are added to (cntT, cntF, cntV = cells written). Shared by windy_rows_kernel (one
 // launch per CA pass) and bulldozer_step_fused_kernel (the whole env step), so both write the same bytes. RD: rows of
 // loads in flight ahead of the row being classified (RD = SH: the whole strip at once), SH: the strip's height.
-template <int NW, int SH, int RD, bool STD>
-__device__ __forceinline__ void windy_rows_strip(const uint8_t* __restrict__ S, uint8_t* __restrict__ Dst, int s0,
-                                                 int H, uint32_t m, uint32_t lofs, uint32_t Ep, uint32_t Tp,
-                                                 uint32_t Fp, int32_t& cntT, int32_t& cntF, int32_t& cntV) {
+template <int NW, int SH, int RD, bool STD, class MaskFn>
+__device__ __forceinline__ void windy_rows_strip_f(const uint8_t* __restrict__ S, uint8_t* __restrict__ Dst, int s0,
+                                                   int H, MaskFn get_mask, uint32_t lofs, uint32_t Ep, uint32_t Tp,
+                                                   uint32_t Fp, int32_t& cntT, int32_t& cntF, int32_t& cntV) {
     constexpr int W = 256 * NW;
     static_assert(RD >= 1 && RD <= SH, "rows in flight: 1 .. SH");
+    // the strip's first rows are requested before the direction mask is known (its draw overlaps their latency)
+    RowRaw<NW> ring[RD];
+    const RowRaw<NW> r_up = load_rowraw<NW>(S, lofs, s0 - 1, H), r_cur = load_rowraw<NW>(S, lofs, s0, H);
+#pragma unroll
+    for (int k = 0; k < RD; ++k) ring[k] = load_rowraw<NW>(S, lofs, s0 + 1 + k, H);
+    const uint32_t m = get_mask();
     // all-ones / zero per direction, made opaque (readfirstlane) so that hipcc keeps `(x & m) | acc` as one
     // v_and_or_b32 per direction instead of turning each mask into a v_cndmask plus a separate or
     auto dm = [&](uint32_t bit) {
@@ -339,10 +345,6 @@ __device__ __forceinline__ void windy_rows_strip(const uint8_t* __restrict__ S, 
 
     const uint32_t codes = (Ep & 0xFFu) | ((Tp & 0xFFu) << 8) | ((Fp & 0xFFu) << 16);
     // ring[k % RD] holds row s0 + 1 + k (k = 0 .. SH): the strip's rows below row s0 up to its lower halo row
-    RowRaw<NW> ring[RD];
-    const RowRaw<NW> r_up = load_rowraw<NW>(S, lofs, s0 - 1, H), r_cur = load_rowraw<NW>(S, lofs, s0, H);
-#pragma unroll
-    for (int k = 0; k < RD; ++k) ring[k] = load_rowraw<NW>(S, lofs, s0 + 1 + k, H);
     RowCls<NW> A = classify_row<NW, STD>(r_up, s0 >= 1, Tp, Fp);
     RowCls<NW> B = classify_row<NW, STD>(r_cur, true, Tp, Fp);
 
@@ -387,6 +389,13 @@ __device__ __forceinline__ void windy_rows_strip(const uint8_t* __restrict__ S, 
         A = B;
         B = C;
     }
+}
+
+template <int NW, int SH, int RD, bool STD>
+__device__ __forceinline__ void windy_rows_strip(const uint8_t* __restrict__ S, uint8_t* __restrict__ Dst, int s0,
+                                                 int H, uint32_t m, uint32_t lofs, uint32_t Ep, uint32_t Tp,
+                                                 uint32_t Fp, int32_t& cntT, int32_t& cntF, int32_t& cntV) {
+    windy_rows_strip_f<NW, SH, RD, STD>(S, Dst, s0, H, [m]() { return m; }, lofs, Ep, Tp, Fp, cntT, cntF, cntV);
 }
 
 template <int NW, bool STD>
@@ -447,8 +456,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
     int32_t* __restrict__ pos, int32_t* __restrict__ counts, uint8_t* __restrict__ hit, double* __restrict__ reward,
     int64_t* __restrict__ steps_elapsed) {
     constexpr int W = 256 * NW;
-    __shared__ int32_t blk_cnt[3];
-    __shared__ uint32_t blk_mask;
+    __shared__ int32_t wave_cnt[16][3];  // per wave (no zeroing, no atomics): summed by thread 0 after the barrier
     const int e = blockIdx.x;
     const int tid = threadIdx.x;
     // ---- every per-env input (wave-uniform addresses: scalar loads), issued together
@@ -474,21 +482,38 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
     const int64_t HW = (int64_t)H * W;
     uint8_t* grid = (odd ? buf1 : buf0) + e * HW;  // the env's grid after this step
     if (n > 0) {
-        if (tid == 0) {
-            blk_mask = windy_mask(wl, nullptr, (uint32_t)p.seed, (uint32_t)(p.seed >> 32), (uint32_t)(p.env_offset + e),
-                                  rs);
-            blk_cnt[0] = blk_cnt[1] = blk_cnt[2] = 0;
-        }
-        __syncthreads();
         const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, nw = (int)(blockDim.x >> 6);
-        const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane((int)blk_mask);
+        // the direction mask (windy_mask, bit for bit) in every wave, no barrier: lane j < 4 draws Philox block j
+        // (directions 2j, 2j+1), two ballots gather the bits; drawn after the strip's first row loads are issued
+        auto get_mask = [&]() -> uint32_t {
+            bool b0 = false, b1 = false;
+            if (lane < 4) {
+                const u32x4 xr = philox4x32_10(u32x4{(uint32_t)lane, (uint32_t)(p.env_offset + e), rs,
+                                                     GCA_TAG_WINDY_ROLL}, (uint32_t)p.seed, (uint32_t)(p.seed >> 32));
+                const int d0 = 2 * lane, d1 = 2 * lane + 1;
+                const int i0 = d0 < 4 ? d0 : d0 + 1, i1 = d1 < 4 ? d1 : d1 + 1;
+                double w0 = wl[0], w1 = wl[0];
+#pragma unroll
+                for (int k = 1; k < 9; ++k) {
+                    w0 = k == i0 ? wl[k] : w0;
+                    w1 = k == i1 ? wl[k] : w1;
+                }
+                b0 = u01_f64(xr.x, xr.y) < w0;
+                b1 = u01_f64(xr.z, xr.w) < w1;
+            }
+            const uint32_t g0 = (uint32_t)__ballot(b0), g1 = (uint32_t)__ballot(b1);
+            uint32_t mm = 0u;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) mm |= (((g0 >> j) & 1u) << (2 * j)) | (((g1 >> j) & 1u) << (2 * j + 1));
+            return (uint32_t)__builtin_amdgcn_readfirstlane((int)mm);
+        };
         const uint8_t* __restrict__ S = grid;
         uint8_t* __restrict__ Dst = (odd ? buf0 : buf1) + e * HW;
         const uint32_t lofs = 4 * NW * (uint32_t)lane;
         int32_t cntT = 0, cntF = 0, cntV = 0;
         for (int s0 = wave * FUSED_SH<NW>; s0 < H; s0 += nw * FUSED_SH<NW>)
-            windy_rows_strip<NW, FUSED_SH<NW>, FUSED_RD<NW>, STD>(S, Dst, s0, H, m, lofs, rep4(p.empty),
-                                                                 rep4(p.tree), rep4(p.fire), cntT, cntF, cntV);
+            windy_rows_strip_f<NW, FUSED_SH<NW>, FUSED_RD<NW>, STD>(S, Dst, s0, H, get_mask, lofs, rep4(p.empty),
+                                                                   rep4(p.tree), rep4(p.fire), cntT, cntF, cntV);
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) {
             cntT += __shfl_xor(cntT, off);
@@ -496,9 +521,9 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
             cntV += __shfl_xor(cntV, off);
         }
         if (lane == 0) {
-            atomicAdd(&blk_cnt[0], cntV - cntT - cntF);
-            atomicAdd(&blk_cnt[1], cntT);
-            atomicAdd(&blk_cnt[2], cntF);
+            wave_cnt[wave][0] = cntV - cntT - cntF;
+            wave_cnt[wave][1] = cntT;
+            wave_cnt[wave][2] = cntF;
         }
         __syncthreads();  // the new grid (every wave's stores) and the counts are complete
         grid = Dst;
@@ -513,9 +538,13 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
     int32_t cE = c0, cT = c1, cF = c2;
     if (n > 0) {
         parity[e] = odd ? 0 : 1;
-        cE = blk_cnt[0];
-        cT = blk_cnt[1];
-        cF = blk_cnt[2];
+        cE = cT = cF = 0;
+        const int nw = (int)(blockDim.x >> 6);
+        for (int w = 0; w < nw; ++w) {
+            cE += wave_cnt[w][0];
+            cT += wave_cnt[w][1];
+            cF += wave_cnt[w][2];
+        }
     }
     // MoveModify (move_modify.py:128-134): Modify at the new position, on the post-CA grid
     pos[2 * e] = row;

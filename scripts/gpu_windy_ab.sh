@@ -1,0 +1,20 @@
+#!/bin/bash
+# Windy env-step A/B of candidate library builds against the in-tree one: the Windy GPU tests on each candidate, then
+# three alternating passes of scripts/ab_windy_env.py. Each step time-limited; a failure ends the run.
+# Usage (GPU box, repo root): bash scripts/gpu_windy_ab.sh <tag> "<variants>"
+TAG=$1; WV=$2
+V=$(pwd)/gym-cellular-automata_amd/gymca_amd/_lib/variants
+O=gpurun_out/$TAG
+mkdir -p $O
+for v in $WV; do
+  GCA_LIB_PATH=$V/$v.so timeout -k 10 600 python -u -m pytest tests/test_gpu_windy.py -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest_$v.log 2>&1
+  RC=$?; echo "pytest exit $RC" >> $O/pytest_$v.log
+  [ $RC -eq 0 ] || exit 22
+done
+for pass in 1 2 3; do
+  echo "windy $pass main $(timeout -k 10 120 python3 -u scripts/ab_windy_env.py)" >> $O/ab.txt || exit 23
+  for v in $WV; do
+    echo "windy $pass $v $(GCA_LIB_PATH=$V/$v.so timeout -k 10 120 python3 -u scripts/ab_windy_env.py)" >> $O/ab.txt || exit 24
+  done
+done
+echo done > $O/done.txt

@@ -45,10 +45,8 @@ def main():
         E = 1024
         env = BatchedForestFireBulldozerEnv(E, N, N, device=device, seed=0x5EED, materialize_obs=False)
         action = torch.zeros((E, 2), dtype=torch.int32, device=device)
-        st = dev.stream_ptr(device)
-
-        def actions():
-            call("gca_random_actions", dev.ptr(action), E, 0, 9, dev.ptr(env.rng_step), st)
+        def actions():  # the stream is read at call time: under capture it is the graph's capture stream
+            call("gca_random_actions", dev.ptr(action), E, 0, 9, dev.ptr(env.rng_step), dev.stream_ptr(device))
 
         def one_step():
             actions()
