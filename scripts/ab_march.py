@@ -10,7 +10,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "gym-cellular-automata_amd")]
 
 
-def main(E=4096, N=256, K=10, reps=5, hidden=False, only=None, rgb_modes=(False, True)):
+def main(E=4096, N=256, K=10, reps=5, hidden=False, only=None, rgb_modes=(False, True), reset_state=False):
     import torch
 
     import bench
@@ -40,14 +40,17 @@ def main(E=4096, N=256, K=10, reps=5, hidden=False, only=None, rgb_modes=(False,
         call(fn + ("_rgb" if rgb else ""), *args, st)
         env.cur = b
 
-    out = {"E": E, "N": N, "K": K, "reps": reps, "hidden": hidden}
+    out = {"E": E, "N": N, "K": K, "reps": reps, "hidden": hidden, "state": "reset" if reset_state else "mid-episode"}
     for rgb in rgb_modes:
         for fn in ("gca_alex_step_packed", "gca_alex_step_march"):
             if only and only not in fn:
                 continue
             times = []
             for _ in range(reps):
-                bench.synthetic_state(env, 0, device)
+                if reset_state:  # the episode-start state (2 fires per env): the quiet-tile copies dominate
+                    env.reset()
+                else:
+                    bench.synthetic_state(env, 0, device)
                 launch(fn, rgb)  # warm-up
                 torch.cuda.synchronize()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -63,11 +66,12 @@ def main(E=4096, N=256, K=10, reps=5, hidden=False, only=None, rgb_modes=(False,
 
 
 if __name__ == "__main__":
-    # --only march|packed: one mapping; --plain: no fused-frame variants; --reps N; --size N (grid side), --envs E
+    # --only march|packed: one mapping; --plain: no fused-frame variants; --reps N; --size N (grid side), --envs E;
+    # --reset: time from the reset state instead of the bench's mid-episode state
     args = sys.argv[1:]
     only = args[args.index("--only") + 1] if "--only" in args else None
     reps = int(args[args.index("--reps") + 1]) if "--reps" in args else 5
     N = int(args[args.index("--size") + 1]) if "--size" in args else 256
     E = int(args[args.index("--envs") + 1]) if "--envs" in args else 4096
     main(E=E, N=N, hidden="--hidden" in args, only=only, reps=reps,
-         rgb_modes=(False,) if "--plain" in args else (False, True))
+         rgb_modes=(False,) if "--plain" in args else (False, True), reset_state="--reset" in args)

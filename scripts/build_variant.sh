@@ -14,5 +14,6 @@ for s in gca_util gca_windy gca_env gca_alex gca_alex_march gca_ds gca_obs gca_p
   /opt/rocm/bin/hipcc $F -c $C/$s.hip -o $B/$s.o &
 done
 wait
+for s in gca_util gca_windy gca_env gca_alex gca_alex_march gca_ds gca_obs gca_pine gca_init; do [ -f $B/$s.o ] || { echo "compile of $s failed" >&2; exit 1; }; done
 /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 $B/*.o -o $O/$NAME.so
 echo $O/$NAME.so
