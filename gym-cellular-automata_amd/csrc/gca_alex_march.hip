@@ -268,8 +268,6 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
         return (r >= 0 && r < H) ? (uint32_t)dE[(uint32_t)r * (W / 16) + ld16] : 0u;
     };
     auto dflags = [&](uint32_t w16) -> uint32_t { return gca_spread4(w16 >> (4 * (lane & 3))); };
-    // RGB row r of the lane's 4 cells (kinds from the new TREE / FIRE nibbles, pre-step dousing flags) through the
-    // wave's LDS row: 48 B per lane in, 3 x 1 KiB contiguous non-temporal stores out
     // The RGB row r of the lane's 4 cells (kinds from the new TREE / FIRE nibbles, pre-step dousing flags) through the
     // wave's LDS row: the 4 colours read back to back (one index byte per cell: 2 * kind + dousing), 3 x 16 B written,
     // then 3 x 1 KiB contiguous non-temporal stores (r03k: two rows per flush, or plain stores, measured slower)
@@ -315,6 +313,33 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
     uint32_t g_init[NF - 1];
 #pragma unroll
     for (int t = 0; t < NF - 1; ++t) g_init[t] = graw(s0 - R - 1 + t);
+    // a quiet tile: the input rows copied (grid, ages when not in place, the frame) and counted; row(i) gives row s0+i
+    auto quiet_copy = [&](auto row) {
+        int cE = 0, cT = 0;
+#pragma unroll
+        for (int i = 0; i < SH; ++i) {
+            const int r = s0 + i;
+            const uint32_t o = (uint32_t)r * W + lc;
+            const uint32_t gw = row(i);
+            __builtin_nontemporal_store(gw, reinterpret_cast<uint32_t*>(gO + o));
+            if (age_in != age_out) *reinterpret_cast<uint2*>(aO + o) = *reinterpret_cast<const uint2*>(aE + o);
+            cE += __builtin_popcount(bytes_eq01(gw, Ep));
+            cT += __builtin_popcount(bytes_eq01(gw, Tp));
+            if (OBS) write_rgb_row(r, gca_eq_nib(gw, Tp), 0u, dflags(draw_bits(r)));
+        }
+        if (act_out && lane == 0) act_out[((size_t)e * strips + s) * NSEG + g] = 0;
+        if (counts) {
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) {
+                cE += __shfl_xor(cE, off);
+                cT += __shfl_xor(cT, off);
+            }
+            if (lane == 0) {
+                if (cE) atomicAdd(counts + 3 * e + 0, cE);
+                if (cT) atomicAdd(counts + 3 * e + 1, cT);
+            }
+        }
+    };
     bool quiet = false;
     if (!HALO && act_out && act_in) {
         const uint8_t* A = act_in + (size_t)e * strips;
@@ -325,10 +350,21 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
             return (v - 0x01010101u) & ~v & 0x80808080u;
         };
         if (__ballot((has_fire(g_init[R]) | has_fire(g_init[R + 1])) != 0u) == 0ull) {  // rows s0 - 1, s0
-            uint32_t f = 0u;
+            uint32_t gq[SH];  // rows s0 .. s0+SH-1, kept for the copy (no second load round trip, r04)
+            gq[0] = g_init[R + 1];
+            uint32_t f = has_fire(graw(s0 + SH));
 #pragma unroll
-            for (int i = 1; i <= SH; ++i) f |= has_fire(graw(s0 + i));
+            for (int i = 1; i < SH; ++i) {
+                gq[i] = graw(s0 + i);
+                f |= has_fire(gq[i]);
+            }
             quiet = __ballot(f != 0u) == 0ull;
+            if constexpr (!HALO) {
+                if (quiet) {
+                    quiet_copy([&](int i) { return gq[i]; });
+                    return;
+                }
+            }
         }
     }
     if constexpr (HALO) {
@@ -352,31 +388,8 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
         for (int w = 0; w < NSEG; ++w) all &= qfl[w];
         quiet = all != 0u;
     }
-    if (quiet) {
-        int cE = 0, cT = 0;
-#pragma unroll 4
-        for (int i = 0; i < SH; ++i) {
-            const int r = s0 + i;
-            const uint32_t o = (uint32_t)r * W + lc;
-            const uint32_t gw = *reinterpret_cast<const uint32_t*>(gE + o);
-            *reinterpret_cast<uint32_t*>(gO + o) = gw;
-            if (age_in != age_out) *reinterpret_cast<uint2*>(aO + o) = *reinterpret_cast<const uint2*>(aE + o);
-            cE += __builtin_popcount(bytes_eq01(gw, Ep));
-            cT += __builtin_popcount(bytes_eq01(gw, Tp));
-            if (OBS) write_rgb_row(r, gca_eq_nib(gw, Tp), 0u, dflags(draw_bits(r)));
-        }
-        if (act_out && lane == 0) act_out[((size_t)e * strips + s) * NSEG + g] = 0;
-        if (counts) {
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) {
-                cE += __shfl_xor(cE, off);
-                cT += __shfl_xor(cT, off);
-            }
-            if (lane == 0) {
-                if (cE) atomicAdd(counts + 3 * e + 0, cE);
-                if (cT) atomicAdd(counts + 3 * e + 1, cT);
-            }
-        }
+    if (quiet) {  // the tile map's verdict, or every segment of a strip quiet (HALO): rows loaded again
+        quiet_copy([&](int i) { return *reinterpret_cast<const uint32_t*>(gE + (uint32_t)(s0 + i) * W + lc); });
         return;
     }
 
