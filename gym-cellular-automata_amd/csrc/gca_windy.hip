@@ -379,9 +379,15 @@ __device__ __forceinline__ void windy_rows_strip_f(const uint8_t* __restrict__ S
         }
         if (Rc < H && t < SH) {
             uint8_t* p = Dst + (uint32_t)Rc * (uint32_t)W + lofs;
+            // W >= 512: non-temporal stores (1024 x 512^2 is 256 MiB per grid, past the Infinity Cache: 105 -> 98 us
+            // per CA-only step, profiles/r04p); W = 256 keeps plain stores (1024 x 256^2 in + out stays cache-resident
+            // across steps; non-temporal: 24 -> 30 us)
+            typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+            typedef uint32_t u4v __attribute__((ext_vector_type(4)));
             if (NW == 1) *reinterpret_cast<uint32_t*>(p) = outw[0];
-            else if (NW == 2) *reinterpret_cast<uint2*>(p) = make_uint2(outw[0], outw[1 % NW]);
-            else *reinterpret_cast<uint4*>(p) = make_uint4(outw[0], outw[1 % NW], outw[2 % NW], outw[3 % NW]);
+            else if (NW == 2) __builtin_nontemporal_store((u2v){outw[0], outw[1 % NW]}, reinterpret_cast<u2v*>(p));
+            else __builtin_nontemporal_store((u4v){outw[0], outw[1 % NW], outw[2 % NW], outw[3 % NW]},
+                                             reinterpret_cast<u4v*>(p));
             cntV += 4 * NW;
             cntT += rowT;
             cntF += rowF;
