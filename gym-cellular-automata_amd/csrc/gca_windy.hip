@@ -577,6 +577,156 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
     if (steps_elapsed) steps_elapsed[e] = se + 1;
 }
 
+// The fused step spread over P workgroups per env (W = 512: one CU's four SIMDs ran a stepping env's 16 waves four deep,
+// ~12 us of VALU; P = 4 workgroups of 4 waves on four CUs). Every part reads the env's inputs and decides the same
+// n; the CA rows are split by strips; the part holding the bulldozer's row applies Modify. The parts meet in one 64-bit
+// atomic per env (E | T | F counts, 20 bits each, the hit bit, and an arrival count in the top 3 bits): the last to
+// arrive writes every per-env output (only then has every part read its inputs) and clears the slot for the next step.
+// `meet`: the caller's per-env slots (zero on entry; every launch leaves them zero). Measured (profiles/r04s-u, one
+// restored mid-episode state, hipGraph of 8 steps with device random actions): 1024 x 512^2 18.3 -> 14.9 us per env
+// step (P = 4; P = 8: 16.5), 1024 x 256^2 14.1 -> 12.7 us (P = 2).
+
+template <int NW, bool STD, int P>
+__global__ __launch_bounds__(256) void bulldozer_step_fused_parts_kernel(
+    gca_bulldozer_params p, const int32_t* __restrict__ action, double* __restrict__ accu, int32_t* __restrict__ steps,
+    uint8_t* __restrict__ done, const double* __restrict__ wind, int64_t wind_stride, uint32_t* __restrict__ rng_step,
+    uint8_t* __restrict__ parity, uint8_t* __restrict__ buf0, uint8_t* __restrict__ buf1, int H,
+    int32_t* __restrict__ pos, int32_t* __restrict__ counts, uint8_t* __restrict__ hit, double* __restrict__ reward,
+    int64_t* __restrict__ steps_elapsed, unsigned long long* __restrict__ meet) {
+    constexpr int W = 256 * NW;
+    constexpr int SHv = (NW == 1 && P >= 4) ? 16 : FUSED_SH<NW>;
+    constexpr int RDv = SHv < FUSED_RD<NW> ? SHv : FUSED_RD<NW>;
+    __shared__ int32_t wave_cnt[4][3];
+    const int e = blockIdx.x / P, part = blockIdx.x - e * P;
+    const int tid = threadIdx.x;
+    const bool was_done = done[e] != 0;
+    const int32_t act0 = action[2 * e], act1 = action[2 * e + 1];
+    const double acc = accu[e];
+    const bool odd = parity[e] != 0;
+    const int32_t prow = pos[2 * e], pcol = pos[2 * e + 1];
+    const int32_t c0 = counts[3 * e + 0], c1 = counts[3 * e + 1], c2 = counts[3 * e + 2];
+    const uint32_t rs = rng_step[e];
+    const int64_t se = steps_elapsed ? steps_elapsed[e] : 0;
+    double wl[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) wl[k] = wind[(int64_t)e * wind_stride + k];
+    const int a0 = clampi_dev(act0, 0, 8), a1s = clampi_dev(act1, 0, 1);
+    const double x = acc + ((p.t_move[a0] + p.t_shoot[a1s]) + p.t_any);
+    const double reps = trunc(x);
+    const int n = was_done ? -1 : (int)reps;
+    int row = prow, col = pcol;
+    move_pos(a0, row, col, H, W, p.up_mask, p.down_mask, p.left_mask, p.right_mask);
+    const int64_t HW = (int64_t)H * W;
+    const int strips = (H + SHv - 1) / SHv, spp = (strips + P - 1) / P;
+    const int s_begin = part * spp, s_end = min(strips, s_begin + spp);
+    uint8_t* grid = (odd ? buf1 : buf0) + e * HW;
+    if (n > 0) {
+        const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+        auto get_mask = [&]() -> uint32_t {
+            bool b0 = false, b1 = false;
+            if (lane < 4) {
+                const u32x4 xr = philox4x32_10(u32x4{(uint32_t)lane, (uint32_t)(p.env_offset + e), rs,
+                                                     GCA_TAG_WINDY_ROLL}, (uint32_t)p.seed, (uint32_t)(p.seed >> 32));
+                const int d0 = 2 * lane, d1 = 2 * lane + 1;
+                const int i0 = d0 < 4 ? d0 : d0 + 1, i1 = d1 < 4 ? d1 : d1 + 1;
+                double w0 = wl[0], w1 = wl[0];
+#pragma unroll
+                for (int k = 1; k < 9; ++k) {
+                    w0 = k == i0 ? wl[k] : w0;
+                    w1 = k == i1 ? wl[k] : w1;
+                }
+                b0 = u01_f64(xr.x, xr.y) < w0;
+                b1 = u01_f64(xr.z, xr.w) < w1;
+            }
+            const uint32_t g0 = (uint32_t)__ballot(b0), g1 = (uint32_t)__ballot(b1);
+            uint32_t mm = 0u;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) mm |= (((g0 >> j) & 1u) << (2 * j)) | (((g1 >> j) & 1u) << (2 * j + 1));
+            return (uint32_t)__builtin_amdgcn_readfirstlane((int)mm);
+        };
+        const uint8_t* __restrict__ S = grid;
+        uint8_t* __restrict__ Dst = (odd ? buf0 : buf1) + e * HW;
+        const uint32_t lofs = 4 * NW * (uint32_t)lane;
+        int32_t cntT = 0, cntF = 0, cntV = 0;
+        for (int s = s_begin + wave; s < s_end; s += 4)
+            windy_rows_strip_f<NW, SHv, RDv, STD>(S, Dst, s * SHv, H, get_mask, lofs, rep4(p.empty),
+                                                           rep4(p.tree), rep4(p.fire), cntT, cntF, cntV);
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            cntT += __shfl_xor(cntT, off);
+            cntF += __shfl_xor(cntF, off);
+            cntV += __shfl_xor(cntV, off);
+        }
+        if (lane == 0) {
+            wave_cnt[wave][0] = cntV - cntT - cntF;
+            wave_cnt[wave][1] = cntT;
+            wave_cnt[wave][2] = cntF;
+        }
+        __syncthreads();
+        grid = Dst;
+    }
+    if (tid != 0) return;
+    // this part's contribution: n > 0 its rows' counts (+ Modify when it holds the bulldozer's row); n == 0 the Modify's
+    // count changes + 1 (owner only); n < 0 nothing
+    int32_t pE = 0, pT = 0, pF = 0;
+    uint32_t h = 0;
+    if (n > 0) {
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            pE += wave_cnt[w][0];
+            pT += wave_cnt[w][1];
+            pF += wave_cnt[w][2];
+        }
+    } else if (n == 0) {
+        pE = pT = pF = 1;
+    }
+    const int owner = min((row / SHv) / spp, P - 1);
+    if (n >= 0 && part == owner && act1) {
+        const int v = grid[(int64_t)row * W + col];
+        const int nv = p.effect[v];
+        if (nv >= 0) {
+            grid[(int64_t)row * W + col] = (uint8_t)nv;
+            h = 1;
+            const int c_old = cell_category(v, p.empty, p.tree, p.fire), c_new = cell_category(nv, p.empty, p.tree, p.fire);
+            if (c_old == 0) pE -= 1; else if (c_old == 1) pT -= 1; else if (c_old == 2) pF -= 1;
+            if (c_new == 0) pE += 1; else if (c_new == 1) pT += 1; else if (c_new == 2) pF += 1;
+        }
+    }
+    if (n == 0 && part != owner) pE = pT = pF = 0;
+    const unsigned long long pk = (unsigned long long)(uint32_t)pE | ((unsigned long long)(uint32_t)pT << 20) |
+                                  ((unsigned long long)(uint32_t)pF << 40) | ((unsigned long long)h << 60) |
+                                  (1ull << 61);
+    const unsigned long long old = atomicAdd(&meet[e], pk);
+    if ((int)(old >> 61) != P - 1) return;  // not the last part to arrive
+    const unsigned long long tot = old + pk;
+    meet[e] = 0ull;
+    steps[e] = n;
+    if (n < 0) {
+        reward[e] = 0.0;
+        return;
+    }
+    accu[e] = x - reps;
+    int32_t cE = (int32_t)(tot & 0xFFFFFu), cT = (int32_t)((tot >> 20) & 0xFFFFFu), cF = (int32_t)((tot >> 40) & 0xFFFFFu);
+    if (n > 0) {
+        parity[e] = odd ? 0 : 1;
+    } else {
+        cE = c0 + cE - 1;
+        cT = c1 + cT - 1;
+        cF = c2 + cF - 1;
+    }
+    const uint8_t hh = (uint8_t)((tot >> 60) & 1u);
+    pos[2 * e] = row;
+    pos[2 * e + 1] = col;
+    counts[3 * e + 0] = cE;
+    counts[3 * e + 1] = cT;
+    counts[3 * e + 2] = cF;
+    hit[e] = hh;
+    reward[e] = (cT + cF) > 0 ? -((double)cF / (double)(cT + cF)) : (double)NAN;
+    done[e] = cF == 0 ? 1 : 0;
+    rng_step[e] = rs + (uint32_t)n;
+    if (steps_elapsed) steps_elapsed[e] = se + 1;
+}
+
 template <int NW>
 static void launch_rows(uint8_t* b0, uint8_t* b1, const uint8_t* parity, const int32_t* steps, int pass,
                         const uint8_t* dm, int E, int H, int empty, int tree, int fire, int32_t* counts,
@@ -664,7 +814,7 @@ extern "C" int gca_bulldozer_step_fused(const gca_bulldozer_params* p, const int
                                         int32_t* steps, uint8_t* done, const double* wind, int64_t wind_stride,
                                         uint32_t* rng_step, uint8_t* parity, uint8_t* buf0, uint8_t* buf1, int H, int W,
                                         int32_t* pos, int32_t* counts, uint8_t* hit, double* reward,
-                                        int64_t* steps_elapsed, int E, void* stream) {
+                                        int64_t* steps_elapsed, uint64_t* meet, int E, void* stream) {
     GCA_CHECK_ARG(p && action && accu && steps && done && wind && rng_step && parity && buf0 && buf1 && pos && counts &&
                       hit && reward && E > 0 && H > 0,
                   "bulldozer_step_fused: null argument or empty batch");
@@ -688,12 +838,25 @@ extern "C" int gca_bulldozer_step_fused(const gca_bulldozer_params* p, const int
     hipLaunchKernelGGL((bulldozer_step_fused_kernel<NWV, STDV>), dim3((unsigned)E), dim3(threads), 0, st, *p, action, \
                        accu, steps, done, wind, wind_stride, rng_step, parity, buf0, buf1, H, pos, counts, hit, reward,   \
                        steps_elapsed)
-    if (W == 256) {
+    // with the caller's meeting slots: P workgroups per env (2 at W = 256, 4 at 512); without: one
+#define GCA_FUSED_PARTS_LAUNCH(NWV, STDV, PV)                                                                     \
+    hipLaunchKernelGGL((bulldozer_step_fused_parts_kernel<NWV, STDV, PV>), dim3((unsigned)E * PV), dim3(256), 0, st, *p, \
+                       action, accu, steps, done, wind, wind_stride, rng_step, parity, buf0, buf1, H, pos, counts, hit,  \
+                       reward, steps_elapsed, (unsigned long long*)meet)
+    if (meet) {
+        GCA_CHECK_ARG((int64_t)E * 4 < ((int64_t)1 << 31), "bulldozer_step_fused: too many envs");
+        if (W == 256) {
+            if (std_codes) GCA_FUSED_PARTS_LAUNCH(1, true, 2); else GCA_FUSED_PARTS_LAUNCH(1, false, 2);
+        } else {
+            if (std_codes) GCA_FUSED_PARTS_LAUNCH(2, true, 4); else GCA_FUSED_PARTS_LAUNCH(2, false, 4);
+        }
+    } else if (W == 256) {
         if (std_codes) GCA_FUSED_LAUNCH(1, true); else GCA_FUSED_LAUNCH(1, false);
     } else {
         if (std_codes) GCA_FUSED_LAUNCH(2, true); else GCA_FUSED_LAUNCH(2, false);
     }
 #undef GCA_FUSED_LAUNCH
+#undef GCA_FUSED_PARTS_LAUNCH
     GCA_CHECK_LAUNCH("bulldozer_step_fused");
     return GCA_OK;
 }

@@ -181,7 +181,7 @@ _SIGNATURES = {
     "gca_bulldozer_post": ([POINTER(BulldozerParams), c_int, P, P, P, P, P, c_int, c_int, P, P, P, P, P, P, c_int, P],
                            c_int),
     "gca_bulldozer_step_fused": ([POINTER(BulldozerParams), P, P, P, P, P, c_int64, P, P, P, P, c_int, c_int, P, P, P,
-                                  P, P, c_int, P], c_int),
+                                  P, P, P, c_int, P], c_int),
     "gca_move_modify": ([POINTER(BulldozerParams), P, P, P, c_int, c_int, P, c_int, P], c_int),
     "gca_alex_prepare_slope": ([P, P, c_int, c_int, c_int, P], c_int),
     "gca_alex_step": ([POINTER(AlexParams), c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P],

@@ -78,6 +78,8 @@ class BatchedForestFireBulldozerEnv:
         w = parse_wind(wind) if isinstance(wind, dict) else np.asarray(wind, dtype=np.float64)
         self.wind = dev.to_device(np.broadcast_to(w.reshape(-1, 9), (E, 9)), torch.float64, self.device)
         self.steps_elapsed = torch.zeros(E, dtype=torch.int64, **kw)
+        # the fused step's per-env meeting slots (gca_bulldozer_step_fused: several workgroups per env), kept zero
+        self._meet = torch.zeros(E, dtype=torch.int64, **kw)
         self._truncated = torch.zeros(E, dtype=torch.bool, **kw)
 
     # ------------------------------------------------------------------ state
@@ -149,7 +151,8 @@ class BatchedForestFireBulldozerEnv:
             call("gca_bulldozer_step_fused", p, dev.ptr(a), dev.ptr(self.accu), dev.ptr(self.steps),
                  dev.ptr(self.done), dev.ptr(self.wind), 9, dev.ptr(self.rng_step), dev.ptr(self.parity),
                  dev.ptr(self.buf[0]), dev.ptr(self.buf[1]), H, W, dev.ptr(self.pos), dev.ptr(self.counts),
-                 dev.ptr(self.hit), dev.ptr(self.reward), dev.ptr(self.steps_elapsed), E, st)
+                 dev.ptr(self.hit), dev.ptr(self.reward), dev.ptr(self.steps_elapsed),
+                 dev.ptr(self._meet) if self._meet is not None else None, E, st)
             # done is 0 / 1 bytes: a bool view, no kernel; truncated is a persistent all-False tensor
             return self._obs(), self.reward, self.done.view(torch.bool), self._truncated, {"hit": self.hit,
                                                                                            "ca_steps": self.steps}

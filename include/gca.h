@@ -120,12 +120,15 @@ int gca_bulldozer_post(const gca_bulldozer_params* p, int last_pass, const int32
  * direction mask and the row-stream CA of gca_windy_step on the env's grid, then gca_bulldozer_post's Move / Modify,
  * counts, reward, done, hit, rng_step and parity; steps_elapsed (nullable) += 1 for live envs. Identical results to
  * the three-kernel sequence. Requires W = 256 or 512, empty = 0 < tree < fire, 16-B aligned buffers and one CA pass
- * at most per env step ((t_move + t_shoot) + t_any < 1 for every action; otherwise GCA_ERR_ARG).            */
+ * at most per env step ((t_move + t_shoot) + t_any < 1 for every action; otherwise GCA_ERR_ARG).
+ * meet (nullable): E 64-bit slots, zero-initialised once by the caller (every launch leaves them zero); with them the
+ * step runs as 2 (W = 256) / 4 (W = 512) workgroups per env that meet in one atomic per env, the last to arrive writing
+ * the env's outputs — the same results; NULL: one workgroup per env. Not shared between concurrent launches.   */
 int gca_bulldozer_step_fused(const gca_bulldozer_params* p, const int32_t* action, double* accu, int32_t* steps,
                              uint8_t* done, const double* wind, int64_t wind_stride, uint32_t* rng_step,
                              uint8_t* parity, uint8_t* buf0, uint8_t* buf1, int H, int W, int32_t* pos,
-                             int32_t* counts, uint8_t* hit, double* reward, int64_t* steps_elapsed, int E,
-                             void* stream);
+                             int32_t* counts, uint8_t* hit, double* reward, int64_t* steps_elapsed, uint64_t* meet,
+                             int E, void* stream);
 
 /* Move then Modify for E envs (move_modify.py:37-134): action[e] = (move, shoot);
  * uses p->up/down/left/right_mask and p->effect; grid may be NULL (Move only); hit nullable. */

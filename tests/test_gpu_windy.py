@@ -300,12 +300,14 @@ def test_sharded_windy_env_equals_unsharded(device, N):
                            torch.nan_to_num(full.reward))
 
 
+@pytest.mark.parametrize("parts", [True, False])
 @pytest.mark.parametrize("N,E,steps", [(256, 48, 120), (512, 16, 120)])
-def test_fused_env_step_equals_three_kernel_step(device, N, E, steps):
-    """gca_bulldozer_step_fused (one launch per env step, a workgroup per env) leaves every env exactly as the
-    gca_bulldozer_pre / gca_windy_step / gca_bulldozer_post sequence does: grids, parity, accu, steps, counts, pos,
-    hit, reward, done, rng_step and steps_elapsed after every step, including envs that finish (no FIRE left) and
-    are stepped again (graceful no-op), and under a hipGraph replay."""
+def test_fused_env_step_equals_three_kernel_step(device, N, E, steps, parts):
+    """gca_bulldozer_step_fused (one launch per env step; `parts`: with the env's meeting slots, 2 / 4 workgroups per
+    env meeting in one atomic, else one workgroup per env) leaves every env exactly as the gca_bulldozer_pre /
+    gca_windy_step / gca_bulldozer_post sequence does: grids, parity, accu, steps, counts, pos, hit, reward, done,
+    rng_step and steps_elapsed after every step, including envs that finish (no FIRE left) and are stepped again
+    (graceful no-op), and under a hipGraph replay; the meeting slots are left zero."""
     import torch
 
     from gymca_amd import _device as dev
@@ -316,6 +318,8 @@ def test_fused_env_step_equals_three_kernel_step(device, N, E, steps):
     envs = [BatchedForestFireBulldozerEnv(E, N, N, device=device, seed=29, fused=f, materialize_obs=False,
                                           p_tree=0.55, p_empty=0.45) for f in (True, False)]
     assert envs[0].fused and not envs[1].fused
+    if not parts:
+        envs[0]._meet = None
     acts = [torch.zeros((E, 2), dtype=torch.int32, device=device) for _ in envs]
     for env in envs:
         env.reset(seed=4)
@@ -355,3 +359,5 @@ def test_fused_env_step_equals_three_kernel_step(device, N, E, steps):
             stepper(1)()
     torch.cuda.synchronize(device)
     check("graph")
+    if parts:
+        assert int(envs[0]._meet.abs().sum().item()) == 0
