@@ -29,6 +29,27 @@ def test_library_exports_every_declared_symbol():
     assert set(names) == set(_lib.EXPORTED_SYMBOLS), set(names) ^ set(_lib.EXPORTED_SYMBOLS)
 
 
+def declared_arities():
+    """{function: number of parameters} from the prototypes in include/gca.h."""
+    src = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    out = {}
+    for m in re.finditer(r"\b(gca_[a-z0-9_]+)\s*\(([^;{]*?)\)\s*;", src):
+        params = m.group(2).strip()
+        out[m.group(1)] = 0 if params in ("", "void") else params.count(",") + 1
+    return out
+
+
+def test_ctypes_signatures_match_the_header_arity():
+    """Every ctypes signature passes as many arguments as the header's prototype takes (a stale table shifts every
+    argument after the difference)."""
+    from gymca_amd import _lib
+
+    ar = declared_arities()
+    assert len(ar) >= 20
+    bad = {n: (len(_lib._SIGNATURES[n][0]), k) for n, k in ar.items() if len(_lib._SIGNATURES[n][0]) != k}
+    assert not bad, bad
+
+
 def test_version_and_error_calls_need_no_gpu():
     from gymca_amd import _lib
 
