@@ -585,7 +585,6 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
 // `meet`: the caller's per-env slots (zero on entry; every launch leaves them zero). Measured (profiles/r04s-u, one
 // restored mid-episode state, hipGraph of 8 steps with device random actions): 1024 x 512^2 18.3 -> 14.9 us per env
 // step (P = 4; P = 8: 16.5), 1024 x 256^2 14.1 -> 12.7 us (P = 2).
-
 template <int NW, bool STD, int P>
 __global__ __launch_bounds__(256) void bulldozer_step_fused_parts_kernel(
     gca_bulldozer_params p, const int32_t* __restrict__ action, double* __restrict__ accu, int32_t* __restrict__ steps,
