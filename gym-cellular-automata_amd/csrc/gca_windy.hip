@@ -444,6 +444,33 @@ __global__ __launch_bounds__(256) void windy_rows_kernel(uint8_t* __restrict__ b
 }
 
 // ------------------------------------------------------------------ the whole ForestFireBulldozer env step, fused
+// The env's direction mask (windy_mask bit for bit) drawn inside one wave, no barrier: lane j < 4 draws Philox block j
+// (directions 2j, 2j+1) against the env's wind, two ballots gather the bits; the result is wave-uniform (an SGPR).
+// Shared by both fused step kernels so their draw order cannot drift apart.
+__device__ __forceinline__ uint32_t wave_windy_mask(const gca_bulldozer_params& p, const double (&wl)[9], int e,
+                                                    uint32_t rs, int lane) {
+    bool b0 = false, b1 = false;
+    if (lane < 4) {
+        const u32x4 xr = philox4x32_10(u32x4{(uint32_t)lane, (uint32_t)(p.env_offset + e), rs, GCA_TAG_WINDY_ROLL},
+                                       (uint32_t)p.seed, (uint32_t)(p.seed >> 32));
+        const int d0 = 2 * lane, d1 = 2 * lane + 1;
+        const int i0 = d0 < 4 ? d0 : d0 + 1, i1 = d1 < 4 ? d1 : d1 + 1;
+        double w0 = wl[0], w1 = wl[0];
+#pragma unroll
+        for (int k = 1; k < 9; ++k) {
+            w0 = k == i0 ? wl[k] : w0;
+            w1 = k == i1 ? wl[k] : w1;
+        }
+        b0 = u01_f64(xr.x, xr.y) < w0;
+        b1 = u01_f64(xr.z, xr.w) < w1;
+    }
+    const uint32_t g0 = (uint32_t)__ballot(b0), g1 = (uint32_t)__ballot(b1);
+    uint32_t mm = 0u;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) mm |= (((g0 >> j) & 1u) << (2 * j)) | (((g1 >> j) & 1u) << (2 * j + 1));
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)mm);
+}
+
 // strips of the fused step: 32 rows with 16 in flight at W = 256 (8 waves per env: four workgroups per CU, so the
 // launch's 1024 workgroups are resident at once), 16 rows with 8 in flight (the rows kernel's) at W = 512 (16 waves)
 template <int NW> constexpr int FUSED_SH = NW == 1 ? 32 : 16;
@@ -491,28 +518,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
         const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, nw = (int)(blockDim.x >> 6);
         // the direction mask (windy_mask, bit for bit) in every wave, no barrier: lane j < 4 draws Philox block j
         // (directions 2j, 2j+1), two ballots gather the bits; drawn after the strip's first row loads are issued
-        auto get_mask = [&]() -> uint32_t {
-            bool b0 = false, b1 = false;
-            if (lane < 4) {
-                const u32x4 xr = philox4x32_10(u32x4{(uint32_t)lane, (uint32_t)(p.env_offset + e), rs,
-                                                     GCA_TAG_WINDY_ROLL}, (uint32_t)p.seed, (uint32_t)(p.seed >> 32));
-                const int d0 = 2 * lane, d1 = 2 * lane + 1;
-                const int i0 = d0 < 4 ? d0 : d0 + 1, i1 = d1 < 4 ? d1 : d1 + 1;
-                double w0 = wl[0], w1 = wl[0];
-#pragma unroll
-                for (int k = 1; k < 9; ++k) {
-                    w0 = k == i0 ? wl[k] : w0;
-                    w1 = k == i1 ? wl[k] : w1;
-                }
-                b0 = u01_f64(xr.x, xr.y) < w0;
-                b1 = u01_f64(xr.z, xr.w) < w1;
-            }
-            const uint32_t g0 = (uint32_t)__ballot(b0), g1 = (uint32_t)__ballot(b1);
-            uint32_t mm = 0u;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) mm |= (((g0 >> j) & 1u) << (2 * j)) | (((g1 >> j) & 1u) << (2 * j + 1));
-            return (uint32_t)__builtin_amdgcn_readfirstlane((int)mm);
-        };
+        auto get_mask = [&]() -> uint32_t { return wave_windy_mask(p, wl, e, rs, lane); };
         const uint8_t* __restrict__ S = grid;
         uint8_t* __restrict__ Dst = (odd ? buf0 : buf1) + e * HW;
         const uint32_t lofs = 4 * NW * (uint32_t)lane;
@@ -584,7 +590,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
 // arrive writes every per-env output (only then has every part read its inputs) and clears the slot for the next step.
 // `meet`: the caller's per-env slots (zero on entry; every launch leaves them zero). Measured (profiles/r04s-u, one
 // restored mid-episode state, hipGraph of 8 steps with device random actions): 1024 x 512^2 18.3 -> 14.9 us per env
-// step (P = 4; P = 8: 16.5), 1024 x 256^2 14.1 -> 12.7 us (P = 2).
+// step (P = 4; P = 8: 16.5), 1024 x 256^2 14.1 -> 12.7 us (P = 2). Only launched for H*W + 1 < 2^20 (the fields' width;
+// gca_bulldozer_step_fused takes the one-workgroup kernel beyond).
 template <int NW, bool STD, int P>
 __global__ __launch_bounds__(256) void bulldozer_step_fused_parts_kernel(
     gca_bulldozer_params p, const int32_t* __restrict__ action, double* __restrict__ accu, int32_t* __restrict__ steps,
@@ -621,28 +628,7 @@ __global__ __launch_bounds__(256) void bulldozer_step_fused_parts_kernel(
     uint8_t* grid = (odd ? buf1 : buf0) + e * HW;
     if (n > 0) {
         const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-        auto get_mask = [&]() -> uint32_t {
-            bool b0 = false, b1 = false;
-            if (lane < 4) {
-                const u32x4 xr = philox4x32_10(u32x4{(uint32_t)lane, (uint32_t)(p.env_offset + e), rs,
-                                                     GCA_TAG_WINDY_ROLL}, (uint32_t)p.seed, (uint32_t)(p.seed >> 32));
-                const int d0 = 2 * lane, d1 = 2 * lane + 1;
-                const int i0 = d0 < 4 ? d0 : d0 + 1, i1 = d1 < 4 ? d1 : d1 + 1;
-                double w0 = wl[0], w1 = wl[0];
-#pragma unroll
-                for (int k = 1; k < 9; ++k) {
-                    w0 = k == i0 ? wl[k] : w0;
-                    w1 = k == i1 ? wl[k] : w1;
-                }
-                b0 = u01_f64(xr.x, xr.y) < w0;
-                b1 = u01_f64(xr.z, xr.w) < w1;
-            }
-            const uint32_t g0 = (uint32_t)__ballot(b0), g1 = (uint32_t)__ballot(b1);
-            uint32_t mm = 0u;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) mm |= (((g0 >> j) & 1u) << (2 * j)) | (((g1 >> j) & 1u) << (2 * j + 1));
-            return (uint32_t)__builtin_amdgcn_readfirstlane((int)mm);
-        };
+        auto get_mask = [&]() -> uint32_t { return wave_windy_mask(p, wl, e, rs, lane); };
         const uint8_t* __restrict__ S = grid;
         uint8_t* __restrict__ Dst = (odd ? buf0 : buf1) + e * HW;
         const uint32_t lofs = 4 * NW * (uint32_t)lane;
@@ -842,7 +828,12 @@ extern "C" int gca_bulldozer_step_fused(const gca_bulldozer_params* p, const int
     hipLaunchKernelGGL((bulldozer_step_fused_parts_kernel<NWV, STDV, PV>), dim3((unsigned)E * PV), dim3(256), 0, st, *p, \
                        action, accu, steps, done, wind, wind_stride, rng_step, parity, buf0, buf1, H, pos, counts, hit,  \
                        reward, steps_elapsed, (unsigned long long*)meet)
-    if (meet) {
+    // the parts meet in 20-bit E / T / F fields of one 64-bit word per env: a field's total reaches H*W (+1 when Modify
+    // moves an uncategorised code to a category), so grids of 2^20 - 1 cells or more take the one-workgroup kernel,
+    // which sums in int32 (W = 256 at H >= 4096, W = 512 at H >= 2048); `meet` is then left untouched
+    // (zero, as the contract requires)
+    const bool parts_fit = (int64_t)H * W + 1 < ((int64_t)1 << 20);
+    if (meet && parts_fit) {
         GCA_CHECK_ARG((int64_t)E * 4 < ((int64_t)1 << 31), "bulldozer_step_fused: too many envs");
         if (W == 256) {
             if (std_codes) GCA_FUSED_PARTS_LAUNCH(1, true, 2); else GCA_FUSED_PARTS_LAUNCH(1, false, 2);

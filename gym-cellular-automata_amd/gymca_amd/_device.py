@@ -29,8 +29,25 @@ def is_device_tensor(x):
     return torch is not None and isinstance(x, torch.Tensor) and x.is_cuda
 
 
+def device_index(device=None):
+    if device is None:
+        return torch.cuda.current_device()
+    if isinstance(device, int):
+        return device
+    device = torch.device(device)
+    return device.index if device.index is not None else torch.cuda.current_device()
+
+
 def stream_ptr(device=None):
-    return torch.cuda.current_stream(device).cuda_stream
+    """The raw hipStream_t of the current stream on `device` (torch's work and hipGraph capture order with it).
+    torch.cuda.current_stream(device).cuda_stream builds a Stream object per call; the raw accessor is the same value
+    at a fraction of the host cost (the batched envs call it on every step)."""
+    return raw_stream(device_index(device))
+
+
+def raw_stream(index):
+    """stream_ptr for a known device index (no device parsing)."""
+    return torch._C._cuda_getCurrentRawStream(index)
 
 
 def ptr(t):

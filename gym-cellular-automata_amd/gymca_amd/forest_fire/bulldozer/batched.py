@@ -24,7 +24,7 @@ import math
 import numpy as np
 
 from ... import _device as dev
-from ..._lib import call
+from ..._lib import SLOT, BoundCall, call
 from ..operators.move_modify import make_params
 from .bulldozer import ACTION_SETS, DEFAULT_WIND, bulldozer_timings, parse_wind
 
@@ -81,6 +81,16 @@ class BatchedForestFireBulldozerEnv:
         # the fused step's per-env meeting slots (gca_bulldozer_step_fused: several workgroups per env), kept zero
         self._meet = torch.zeros(E, dtype=torch.int64, **kw)
         self._truncated = torch.zeros(E, dtype=torch.bool, **kw)
+        # the eager step's host path: persistent outputs and pre-bound C-ABI calls, so a step is
+        # one action check, one raw-stream read and one prepared ctypes call
+        self._dev_index = dev.device_index(self.device)
+        self._act_buf = torch.zeros((E, 2), dtype=torch.int32, **kw)
+        self._act_src = None
+        self._done_bool = self.done.view(torch.bool)
+        self._info = {"hit": self.hit, "ca_steps": self.steps}
+        self._ctx = {"wind": self.wind, "position": self.pos, "time": self.accu}
+        self._fused_call = self._bound_meet = None
+        self._sample_call = None
 
     # ------------------------------------------------------------------ state
     def grids(self):
@@ -132,30 +142,68 @@ class BatchedForestFireBulldozerEnv:
         return self._obs(), {"hit": self.hit}
 
     def _obs(self):
-        ctx = {"wind": self.wind, "position": self.pos, "time": self.accu}
-        return (self.grids() if self.materialize_obs else None), ctx
+        return (self.grids() if self.materialize_obs else None), self._ctx
+
+    def _action(self, action):
+        """action as a contiguous int32 (E, 2) device tensor: the caller's own tensor when it already is one (checked
+        once per tensor object), else converted into the env's action buffer."""
+        import torch
+
+        if action is self._act_src:
+            return action
+        E = self.num_envs
+        if (type(action) is torch.Tensor and action.is_cuda and action.dtype == torch.int32 and action.shape == (E, 2)
+                and action.is_contiguous() and action.device == self.device):
+            self._act_src = action
+            return action
+        src = action if dev.is_device_tensor(action) else torch.as_tensor(np.asarray(action))
+        self._act_buf.copy_(src.reshape(E, 2))
+        return self._act_buf
+
+    def _bind_fused(self):
+        E, H, W = self.num_envs, self.nrows, self.ncols
+        meet = self._meet
+        self._fused_call = BoundCall(
+            "gca_bulldozer_step_fused", self.params, SLOT, dev.ptr(self.accu), dev.ptr(self.steps), dev.ptr(self.done),
+            dev.ptr(self.wind), 9, dev.ptr(self.rng_step), dev.ptr(self.parity), dev.ptr(self.buf[0]),
+            dev.ptr(self.buf[1]), H, W, dev.ptr(self.pos), dev.ptr(self.counts), dev.ptr(self.hit),
+            dev.ptr(self.reward), dev.ptr(self.steps_elapsed), dev.ptr(meet) if meet is not None else None, E, SLOT)
+        self._bound_meet = meet
+        return self._fused_call
+
+    def sample_actions(self, out=None, tag=9):
+        """Uniform random actions for every env on the device -- the batched `action_space.sample()` (move in [0, 9),
+        shoot in {0, 1}; Philox keyed by (tag, global env id, the env's rng_step)) -- into `out` (a contiguous int32
+        (E, 2) device tensor) or the env's action buffer. Returns the tensor."""
+        out = self._act_buf if out is None else out
+        if self._sample_call is None or self._sample_call[0] is not out or self._sample_call[1] != tag:
+            if not (dev.is_device_tensor(out) and out.is_contiguous() and out.numel() == 2 * self.num_envs
+                    and out.element_size() == 4 and not out.is_floating_point()):
+                raise ValueError("sample_actions: out must be a contiguous int32 (E, 2) device tensor")
+            self._sample_call = (out, tag, BoundCall("gca_random_actions", dev.ptr(out), self.num_envs,
+                                                     self.env_offset, tag, dev.ptr(self.rng_step), SLOT))
+        self._sample_call[2](dev.raw_stream(self._dev_index))
+        return out
 
     # ------------------------------------------------------------------ step
     def step(self, action):
         """action: (E, 2) int (move in [0,9), shoot in {0,1}); device tensor or numpy. Returns (obs, reward,
         terminated, truncated, info) as device tensors that the next step overwrites in place (terminated is a bool
-        view of `done`, truncated a persistent all-False tensor: no kernel launch per step); clone to keep them."""
+        view of `done`, truncated a persistent all-False tensor, info one persistent dict: no kernel launch and no
+        allocation per step); clone to keep them. A contiguous int32 (E, 2) device action is used as it is."""
+        a = self._action(action)
+        if self.fused:
+            fc = self._fused_call if self._bound_meet is self._meet else None
+            if fc is None:
+                fc = self._bind_fused()
+            fc(a.data_ptr(), dev.raw_stream(self._dev_index))
+            # done is 0 / 1 bytes: a bool view, no kernel; truncated is a persistent all-False tensor
+            return self._obs(), self.reward, self._done_bool, self._truncated, self._info
         import torch
 
         E, H, W = self.num_envs, self.nrows, self.ncols
-        a = action if dev.is_device_tensor(action) else torch.as_tensor(np.asarray(action), device=self.device)
-        a = a.to(torch.int32).reshape(E, 2).contiguous()
         st = dev.stream_ptr(self.device)
         p = self.params
-        if self.fused:
-            call("gca_bulldozer_step_fused", p, dev.ptr(a), dev.ptr(self.accu), dev.ptr(self.steps),
-                 dev.ptr(self.done), dev.ptr(self.wind), 9, dev.ptr(self.rng_step), dev.ptr(self.parity),
-                 dev.ptr(self.buf[0]), dev.ptr(self.buf[1]), H, W, dev.ptr(self.pos), dev.ptr(self.counts),
-                 dev.ptr(self.hit), dev.ptr(self.reward), dev.ptr(self.steps_elapsed),
-                 dev.ptr(self._meet) if self._meet is not None else None, E, st)
-            # done is 0 / 1 bytes: a bool view, no kernel; truncated is a persistent all-False tensor
-            return self._obs(), self.reward, self.done.view(torch.bool), self._truncated, {"hit": self.hit,
-                                                                                           "ca_steps": self.steps}
         call("gca_bulldozer_pre", p, dev.ptr(a), dev.ptr(self.accu), dev.ptr(self.steps), dev.ptr(self.done),
              dev.ptr(self.wind), 9, dev.ptr(self.rng_step), dev.ptr(self.dir_mask), dev.ptr(self.counts), E, st)
         P = self.max_passes
@@ -171,8 +219,7 @@ class BatchedForestFireBulldozerEnv:
              dev.ptr(self.buf[0]), dev.ptr(self.buf[1]), H, W, dev.ptr(self.pos), dev.ptr(self.counts),
              dev.ptr(self.rng_step), dev.ptr(self.done), dev.ptr(self.hit), dev.ptr(self.reward), E, st)
         self.steps_elapsed += (self.steps >= 0).to(torch.int64)
-        return self._obs(), self.reward, self.done.view(torch.bool), self._truncated, {"hit": self.hit,
-                                                                                       "ca_steps": self.steps}
+        return self._obs(), self.reward, self._done_bool, self._truncated, self._info
 
     def ca_step_all(self, dir_mask=None):
         """One forced WindyForestFire step of every env (bench 'CA-only' mode, steps[E] = 1)."""

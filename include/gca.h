@@ -123,7 +123,8 @@ int gca_bulldozer_post(const gca_bulldozer_params* p, int last_pass, const int32
  * at most per env step ((t_move + t_shoot) + t_any < 1 for every action; otherwise GCA_ERR_ARG).
  * meet (nullable): E 64-bit slots, zero-initialised once by the caller (every launch leaves them zero); with them the
  * step runs as 2 (W = 256) / 4 (W = 512) workgroups per env that meet in one atomic per env, the last to arrive writing
- * the env's outputs — the same results; NULL: one workgroup per env. Not shared between concurrent launches.   */
+ * the env's outputs — the same results; NULL: one workgroup per env. Not shared between concurrent launches. The
+ * slots pack 20-bit counts, so grids with H*W + 1 >= 2^20 cells ignore `meet` and run one workgroup per env.   */
 int gca_bulldozer_step_fused(const gca_bulldozer_params* p, const int32_t* action, double* accu, int32_t* steps,
                              uint8_t* done, const double* wind, int64_t wind_stride, uint32_t* rng_step,
                              uint8_t* parity, uint8_t* buf0, uint8_t* buf1, int H, int W, int32_t* pos,

@@ -115,3 +115,25 @@ def test_struct_layouts_match_the_header(tmp_path):
             assert getattr(py[t], f).offset == int(val), key
         else:
             assert ctypes.sizeof(py[key]) == int(val), key
+
+
+def test_bound_call_converts_once_and_checks_arity():
+    """_lib.BoundCall (the batched envs' pre-bound step call): every argument converted to its declared ctypes type
+    at bind time, structs by reference, SLOT positions rebound per call; wrong arities refused before any call."""
+    from gymca_amd import _lib
+
+    p = _lib.BulldozerParams()
+    args = [p, _lib.SLOT] + [0x1000 + 16 * i for i in range(4)] + [9] + [0x2000 + 16 * i for i in range(4)] + \
+        [256, 256] + [0x3000 + 16 * i for i in range(6)] + [1024, _lib.SLOT]
+    bc = _lib.BoundCall("gca_bulldozer_step_fused", *args)
+    assert len(bc._slots) == 2 and len(bc._args) == len(args)
+    assert isinstance(bc._args[6], ctypes.c_int64) and bc._args[6].value == 9
+    assert isinstance(bc._args[2], ctypes.c_void_p) and bc._args[2].value == 0x1000
+    p.t_any = 0.25  # bound by reference: the call sees later edits of the struct
+    assert ctypes.cast(bc._args[0], ctypes.POINTER(_lib.BulldozerParams)).contents.t_any == 0.25
+    with pytest.raises(TypeError):
+        _lib.BoundCall("gca_bulldozer_step_fused", *args[:-1])
+    with pytest.raises(TypeError):
+        _lib.BoundCall("gca_bulldozer_step_fused", _lib.SLOT, *args[1:])
+    with pytest.raises(TypeError):
+        bc(0x4000)  # two per-call values expected

@@ -301,8 +301,13 @@ def test_sharded_windy_env_equals_unsharded(device, N):
 
 
 @pytest.mark.parametrize("parts", [True, False])
-@pytest.mark.parametrize("N,E,steps", [(256, 48, 120), (512, 16, 120)])
-def test_fused_env_step_equals_three_kernel_step(device, N, E, steps, parts):
+@pytest.mark.parametrize("H,W,E,steps", [(256, 256, 48, 120), (512, 512, 16, 120),
+                                         # strips that do not split evenly over the parts -- a last
+                                         # strip only partly filled (48, 100 at 256; 48, 80 at 512), parts with no
+                                         # strip at all (16 and 80 at 512), the bulldozer in the last strip
+                                         (48, 256, 32, 120), (100, 256, 32, 120), (16, 512, 16, 120),
+                                         (48, 512, 16, 120), (80, 512, 16, 120)])
+def test_fused_env_step_equals_three_kernel_step(device, H, W, E, steps, parts):
     """gca_bulldozer_step_fused (one launch per env step; `parts`: with the env's meeting slots, 2 / 4 workgroups per
     env meeting in one atomic, else one workgroup per env) leaves every env exactly as the gca_bulldozer_pre /
     gca_windy_step / gca_bulldozer_post sequence does: grids, parity, accu, steps, counts, pos, hit, reward, done,
@@ -315,19 +320,21 @@ def test_fused_env_step_equals_three_kernel_step(device, N, E, steps, parts):
     from gymca_amd.forest_fire.bulldozer import BatchedForestFireBulldozerEnv
     from gymca_amd.graph import StepGraph
 
-    envs = [BatchedForestFireBulldozerEnv(E, N, N, device=device, seed=29, fused=f, materialize_obs=False,
+    envs = [BatchedForestFireBulldozerEnv(E, H, W, device=device, seed=29, fused=f, materialize_obs=False,
                                           p_tree=0.55, p_empty=0.45) for f in (True, False)]
     assert envs[0].fused and not envs[1].fused
     if not parts:
         envs[0]._meet = None
     acts = [torch.zeros((E, 2), dtype=torch.int32, device=device) for _ in envs]
+    # the bulldozer starts in the grid's last strip (the part that owns Modify is the last one with rows)
+    start = np.stack([np.full(E, H - 2), (np.arange(E) * 37) % W], axis=1)
     for env in envs:
-        env.reset(seed=4)
+        env.reset(seed=4, positions=start)
         # a few envs start without FIRE: done after their first step, then stepped as finished envs
         g = env.grids()
         g[: E // 8][g[: E // 8] == 25] = 3
         env.buf[0].copy_(g)
-        call("gca_count_cells", dev.ptr(env.buf[0]), E, N, N, 0, 3, 25, dev.ptr(env.counts), dev.stream_ptr(device))
+        call("gca_count_cells", dev.ptr(env.buf[0]), E, H, W, 0, 3, 25, dev.ptr(env.counts), dev.stream_ptr(device))
 
     names = ("parity", "accu", "steps", "counts", "pos", "hit", "reward", "done", "rng_step", "steps_elapsed")
 
@@ -361,3 +368,132 @@ def test_fused_env_step_equals_three_kernel_step(device, N, E, steps, parts):
     check("graph")
     if parts:
         assert int(envs[0]._meet.abs().sum().item()) == 0
+
+
+def _dense_state(env, device, seed, p_fire):
+    """A mid-episode-like state written into env: fires sprinkled at rate p_fire, accu uniform in [0, 1) (so a
+    share of the envs steps the CA on every env step), counts recomputed."""
+    import torch
+
+    from gymca_amd import _device as dev
+    from gymca_amd._lib import call
+
+    gen = torch.Generator(device=device).manual_seed(seed)
+    g = env.grids()
+    g[torch.rand(g.shape, device=device, generator=gen) < p_fire] = 25
+    env.buf[0].copy_(g)
+    env.parity.zero_()
+    env.accu.copy_(torch.rand(env.num_envs, device=device, generator=gen, dtype=torch.float64))
+    call("gca_count_cells", dev.ptr(env.buf[0]), env.num_envs, env.nrows, env.ncols, 0, 3, 25, dev.ptr(env.counts),
+         dev.stream_ptr(device))
+
+
+@pytest.mark.parametrize("N", [256, 512])
+def test_fused_parts_at_bench_batch(device, N):
+    """the bench's own Windy env step -- E = 1024, the parts kernel (2 / 4 workgroups per env
+    meeting in one atomic) -- bit-identical to the one-workgroup fused kernel (meet = NULL) and to the three-kernel
+    step, every state tensor after every one of 60 env steps with device random actions from a dense mid-episode state;
+    the meeting slots are zero afterwards."""
+    import torch
+
+    from gymca_amd import _device as dev
+    from gymca_amd._lib import call
+    from gymca_amd.forest_fire.bulldozer import BatchedForestFireBulldozerEnv
+
+    E = 1024
+    envs = [BatchedForestFireBulldozerEnv(E, N, N, device=device, seed=41, fused=f, materialize_obs=False)
+            for f in (True, True, False)]
+    envs[1]._meet = None
+    for env in envs:
+        env.reset(seed=8)
+        _dense_state(env, device, seed=123, p_fire=0.05)
+    acts = [torch.zeros((E, 2), dtype=torch.int32, device=device) for _ in envs]
+    names = ("parity", "accu", "steps", "counts", "pos", "hit", "reward", "done", "rng_step", "steps_elapsed")
+    ca_steps = 0
+    for s in range(60):
+        for env, a in zip(envs, acts):
+            call("gca_random_actions", dev.ptr(a), E, 0, 19, dev.ptr(env.rng_step), dev.stream_ptr(device))
+            env.step(a)
+        ca_steps += int((envs[0].steps > 0).sum().item())
+        ref = envs[2]
+        for k in (0, 1):
+            assert torch.equal(envs[k].grids(), ref.grids()), f"grids, env object {k}, step {s}"
+            for name in names:
+                ta, tb = getattr(envs[k], name), getattr(ref, name)
+                assert torch.equal(torch.nan_to_num(ta), torch.nan_to_num(tb)), f"{name}, env object {k}, step {s}"
+    assert ca_steps > 60 * E // 40  # the CA really ran on many envs per step
+    assert int(envs[0]._meet.abs().sum().item()) == 0
+
+
+@pytest.mark.parametrize("H,W", [(8192, 256), (2048, 512), (2047, 512)])
+def test_fused_parts_counts_on_tall_grids(device, H, W):
+    """ADVICE / VERDICT r04: the parts kernel packs E / T / F counts into 20-bit fields. At 8192 x 256 and 2048 x 512
+    (2^21 / 2^20 cells, an all-TREE grid) a packed field would carry into the next: gca_bulldozer_step_fused must take
+    the one-workgroup kernel there (meet untouched); at 2047 x 512 (the largest parts grid) the packed counts sit just
+    below 2^20. Counts, reward, done and grids equal the three-kernel step over 12 forced CA steps."""
+    import torch
+
+    from gymca_amd import _device as dev
+    from gymca_amd._lib import call
+    from gymca_amd.forest_fire.bulldozer import BatchedForestFireBulldozerEnv
+
+    E = 2
+    envs = [BatchedForestFireBulldozerEnv(E, H, W, device=device, seed=7, fused=f, materialize_obs=False,
+                                          p_tree=1.0, p_empty=0.0) for f in (True, False)]
+    assert envs[0].fused
+    acts = [torch.zeros((E, 2), dtype=torch.int32, device=device) for _ in envs]
+    for env, a in zip(envs, acts):
+        env.reset(seed=3)  # all TREE + the reset's one FIRE per env
+        g = env.grids()
+        g[:, H // 2, : W // 2] = 25  # a fire line: burns for many steps
+        env.buf[0].copy_(g)
+        call("gca_count_cells", dev.ptr(env.buf[0]), E, H, W, 0, 3, 25, dev.ptr(env.counts), dev.stream_ptr(device))
+        a[:, 0] = 4  # stay
+        a[:, 1] = 1  # shoot: Modify TREE -> EMPTY at the bulldozer
+    assert int(envs[1].counts[:, 1].max().item()) >= H * W - W  # a TREE count near H*W
+    for s in range(12):
+        for env, a in zip(envs, acts):
+            env.accu.fill_(0.9999)  # every env steps the CA on this env step
+            env.step(a)
+        fused, three = envs
+        assert int(fused.steps.min().item()) == 1
+        assert torch.equal(fused.grids(), three.grids()), f"grids, step {s}"
+        for name in ("counts", "reward", "done", "hit", "pos", "parity", "rng_step"):
+            ta, tb = getattr(fused, name), getattr(three, name)
+            assert torch.equal(torch.nan_to_num(ta), torch.nan_to_num(tb)), f"{name}, step {s}"
+        # counts are the grid's own
+        g = fused.grids()
+        exp = torch.stack([(g == v).sum(dim=(1, 2)) for v in (0, 3, 25)], dim=1).to(torch.int32)
+        assert torch.equal(fused.counts, exp), f"counts vs grid, step {s}"
+    assert int(envs[0]._meet.abs().sum().item()) == 0
+
+
+def test_eager_step_action_forms_and_sampler(device):
+    """The eager host path (pre-bound call): env.sample_actions == gca_random_actions with the same
+    tag; the same actions given as the caller's int32 device tensor, an int64 device tensor, a numpy array or a flat
+    (2E,) tensor step every env identically; the caller's int32 tensor is used in place (no copy)."""
+    import torch
+
+    from gymca_amd import _device as dev
+    from gymca_amd._lib import call
+    from gymca_amd.forest_fire.bulldozer import BatchedForestFireBulldozerEnv
+
+    E, N = 64, 256
+    envs = [BatchedForestFireBulldozerEnv(E, N, N, device=device, seed=5, materialize_obs=False) for _ in range(4)]
+    for env in envs:
+        env.reset(seed=2)
+        _dense_state(env, device, seed=9, p_fire=0.05)
+    mine = torch.zeros((E, 2), dtype=torch.int32, device=device)
+    ref = torch.zeros((E, 2), dtype=torch.int32, device=device)
+    for s in range(40):
+        call("gca_random_actions", dev.ptr(ref), E, 0, 21, dev.ptr(envs[0].rng_step), dev.stream_ptr(device))
+        got = envs[0].sample_actions(mine, 21)
+        assert got is mine and torch.equal(mine, ref)
+        forms = [mine, mine.to(torch.int64), mine.cpu().numpy(), mine.reshape(-1).clone()]
+        for env, a in zip(envs, forms):
+            env.step(a)
+        assert envs[0]._act_src is mine
+        for env in envs[1:]:
+            assert torch.equal(env.grids(), envs[0].grids()), f"step {s}"
+            for name in ("pos", "accu", "counts", "rng_step", "hit", "done"):
+                assert torch.equal(getattr(env, name), getattr(envs[0], name)), f"{name} step {s}"
