@@ -654,7 +654,6 @@ __global__ __launch_bounds__(NT, WGS) void alex_step_kernel(
     const uint32_t k0 = (uint32_t)p.seed, k1 = (uint32_t)(p.seed >> 32);
     const uint32_t env_id = (uint32_t)(p.env_offset + e);
     const bool want_prob = PROB && prob_out != nullptr;
-    const uint32_t lin0 = lo;  // cell index of cell 0 within the env
 
     const uint32_t fireB = (nbw[1] >> 1) & 0xFFFFu;
     auto dir_bits = [&](int d) -> uint32_t { return dir_bits_of(nbw, d); };
@@ -802,40 +801,58 @@ __global__ __launch_bounds__(NT, WGS) void alex_step_kernel(
             NA[pp] = __builtin_amdgcn_perm(n1, n0, 0x05040100u);
         }
     } else {
-        // Philox block for cell index pair lin>>1; word pair (2h, 2h+1) for h = lin & 1.
-        // burn iff u < 1 - qn  <=>  (main >> 8) < (1 - qn) * 2^24 (exact power-of-two scaling);
-        // grow iff u < p_tree. Cells that need no draw cannot change through them (qn = 1 -> 1-qn = 0).
+        // Philox (r05): one block per group of 4 cells (r, 4g .. 4g+3), counter r * ceil(W/4) + g (the lane's 16
+        // cells are 4 whole groups: cbase % 16 == 0; the march kernel and the C oracle use the same groups); cell j
+        // of a group tests word j: burn iff u < 1 - qn <=> (word >> 8) < (1 - qn) * 2^24 (exact power-of-two
+        // scaling); grow iff u < p_tree. Cells that need no draw cannot change through them (qn = 1 -> 1-qn = 0).
+        // The group's first new fire takes randint of its spare word (the words' low bytes, read by no decision),
+        // the 2nd..4th words 0..2 of the group's ALXA block (rare: only computed when some lane needs it).
         const uint32_t needB = okB & ((treeB & anyfire) | (p.p_tree > 0.0f ? emptyB : 0u));
         const float pt24 = __fmul_rn(p.p_tree, 16777216.0f);
-        const bool odd = !FAST && (lin0 & 1u);  // FAST: W even -> every lane's first cell is even
-        uint32_t Dt = 0u, Dg = 0u;
+        const uint32_t grp0 = (uint32_t)r * (((uint32_t)W + 3u) >> 2) + ((uint32_t)cbase >> 2);
+        uint32_t Dt = 0u, Dg = 0u, spare[4];
 #pragma unroll
-        for (int pp = 0; pp < 8; ++pp) {
-            const uint32_t nd = (needB >> (2 * pp)) & 3u;
-            const uint32_t cA = (lin0 + (uint32_t)(2 * pp)) >> 1;
-            u32x4 XA = u32x4{0u, 0u, 0u, 0u}, XB = u32x4{0u, 0u, 0u, 0u};
-            uint32_t m0, m1, a0, a1;
-            if (!odd) {
-                if (nd) XA = philox4x32_10(u32x4{cA, env_id, step, GCA_TAG_ALEX_CELL}, k0, k1);
-                m0 = XA.x; a0 = XA.y; m1 = XA.z; a1 = XA.w;
-            } else {
-                if (nd & 1u) XA = philox4x32_10(u32x4{cA, env_id, step, GCA_TAG_ALEX_CELL}, k0, k1);
-                if (nd & 2u) XB = philox4x32_10(u32x4{cA + 1u, env_id, step, GCA_TAG_ALEX_CELL}, k0, k1);
-                m0 = XA.z; a0 = XA.w; m1 = XB.x; a1 = XB.y;
+        for (int gq = 0; gq < 4; ++gq) {
+            const uint32_t nd = (needB >> (4 * gq)) & 0xFu;
+            u32x4 X = u32x4{0u, 0u, 0u, 0u};
+            if (nd) X = philox4x32_10(u32x4{grp0 + (uint32_t)gq, env_id, step, GCA_TAG_ALEX_CELL}, k0, k1);
+            const uint32_t mw[4] = {X.x, X.y, X.z, X.w};
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int pp = 2 * gq + h;
+                const f2 thr = ((f2){1.0f, 1.0f} - qn2[pp]) * (f2){16777216.0f, 16777216.0f};
+                const float u0 = (float)(mw[2 * h] >> 8), u1 = (float)(mw[2 * h + 1] >> 8);
+                Dt = push_lt(Dt, u0, thr.x);
+                Dt = push_lt(Dt, u1, thr.y);
+                Dg = push_lt(Dg, u0, pt24);
+                Dg = push_lt(Dg, u1, pt24);
             }
-            const f2 thr = ((f2){1.0f, 1.0f} - qn2[pp]) * (f2){16777216.0f, 16777216.0f};
-            const float u0 = (float)(m0 >> 8), u1 = (float)(m1 >> 8);
-            Dt = push_lt(Dt, u0, thr.x);
-            Dt = push_lt(Dt, u1, thr.y);
-            Dg = push_lt(Dg, u0, pt24);
-            Dg = push_lt(Dg, u1, pt24);
-            const uint32_t n0 = (uint32_t)randint_ms(a0, p.age_lo, p.age_hi);
-            const uint32_t n1 = (uint32_t)randint_ms(a1, p.age_lo, p.age_hi);
-            NA[pp] = __builtin_amdgcn_perm(n1, n0, 0x05040100u);
+            spare[gq] = __builtin_amdgcn_perm(__builtin_amdgcn_perm(X.w, X.z, 0x0c0c0400u),
+                                              __builtin_amdgcn_perm(X.y, X.x, 0x0c0c0400u), 0x05040100u);
             __builtin_amdgcn_sched_barrier(0);  // one Philox block in flight per lane (2 or 4 interleaved: same time, r02h)
         }
         burn = (__builtin_bitreverse32(Dt) >> 16) & treeB & okB;
         grow = (__builtin_bitreverse32(Dg) >> 16) & emptyB & okB;
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq) {
+            const uint32_t n0 = (uint32_t)randint_ms(spare[gq], p.age_lo, p.age_hi);
+            NA[2 * gq] = NA[2 * gq + 1] = __builtin_amdgcn_perm(n0, n0, 0x05040100u);
+            const uint32_t b4 = (burn >> (4 * gq)) & 0xFu;
+            if (__ballot((b4 & (b4 - 1u)) != 0u) != 0ull) {  // a lane with 2+ new fires in this group
+                const u32x4 Y = philox4x32_10(u32x4{grp0 + (uint32_t)gq, env_id, step, GCA_TAG_ALEX_AGE}, k0, k1);
+                const uint32_t nk[4] = {n0, (uint32_t)randint_ms(Y.x, p.age_lo, p.age_hi),
+                                        (uint32_t)randint_ms(Y.y, p.age_lo, p.age_hi),
+                                        (uint32_t)randint_ms(Y.z, p.age_lo, p.age_hi)};
+                uint32_t a[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t rank = (uint32_t)__builtin_popcount(b4 & ((1u << j) - 1u));
+                    a[j] = rank == 0 ? nk[0] : (rank == 1 ? nk[1] : (rank == 2 ? nk[2] : nk[3]));
+                }
+                NA[2 * gq] = __builtin_amdgcn_perm(a[1], a[0], 0x05040100u);
+                NA[2 * gq + 1] = __builtin_amdgcn_perm(a[3], a[2], 0x05040100u);
+            }
+        }
     }
 
     // ---- the rule on masks: TREE -> FIRE (burn), EMPTY -> TREE (grow), FIRE -> EMPTY (age <= 1)

@@ -488,13 +488,14 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
     const uint32_t pu0 = (uint32_t)(pq1 >> 32) ^ env_id ^ k0;  // word 0 after round 1 (uniform)
     const uint64_t pq2 = (uint64_t)PM0 * pu0;                   // round 2's word-0 product (uniform)
     const uint32_t pkc = (uint32_t)GCA_TAG_ALEX_CELL ^ k1;      // round 1: word 2 = hi0 ^ tag ^ k1
+    const uint32_t pkc_age = (uint32_t)GCA_TAG_ALEX_AGE ^ k1;   // the same for the rare second block (tag ALXA)
     const uint32_t pka = (uint32_t)pq1 ^ (k0 + PW0);            // round 2: word 0 = hi1 ^ (word 1 = lo(M1 step)) ^ key
     const uint32_t pkb = (uint32_t)(pq2 >> 32) ^ (k1 + PW1);    // round 2: word 2 = hi(M0 pu0) ^ (word 3 = lo0) ^ key
     const uint32_t pl2 = (uint32_t)pq2;                         // round 2: word 3 = lo(M0 pu0)
-    auto philox_cell = [&](uint32_t x0, uint32_t rk0, uint32_t rk1) -> u32x4 {
+    auto philox_cell = [&](uint32_t x0, uint32_t rk0, uint32_t rk1, uint32_t ktag) -> u32x4 {
         const uint64_t p0 = (uint64_t)PM0 * x0;  // round 1
         const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
-        const uint64_t p1 = (uint64_t)PM1 * (hi0 ^ pkc);  // round 2 (word 2 after round 1)
+        const uint64_t p1 = (uint64_t)PM1 * (hi0 ^ ktag);  // round 2 (word 2 after round 1)
         u32x4 c = u32x4{(uint32_t)(p1 >> 32) ^ pka, (uint32_t)p1, lo0 ^ pkb, pl2};
 #pragma unroll
         for (int i = 2; i < 10; ++i) {  // rounds 3..10 as philox4x32_10, keys (k0 + i W0, k1 + i W1)
@@ -821,38 +822,61 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
             for (int k = 0; k < 3; ++k) SN[k] = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
         }
 
-        // ---- draws: one Philox block per cell pair (cells 4l, 4l+1 and 4l+2, 4l+3), as gca_alex.hip
+        // ---- draws (r05): one Philox block per lane-row -- the lane's 4 cells are the group (r, 4l .. 4l+3), counter
+        //      r * W/4 + l = lin0 >> 2 (gca.h GCA_TAG_ALEX_CELL; as gca_alex.hip and the C oracle). Cell j's burn / grow
+        //      uniform is word j's high 24 bits; the low bytes, which no decision reads, make the spare word whose
+        //      randint is the age of the lane's first new fire. Until r04 every cell pair took a block (its second
+        //      word the cell's age draw): 2 blocks per lane-row, ~100 of ~640 VALU per wave-row
         const uint32_t needB = (treeB & anyfire) | (GROW ? emptyB : 0u);
         const uint32_t lin0 = (uint32_t)r * W + lc;
         uint32_t burn = 0u, grow = 0u, NA[2];
         // every lane draws when any lane of the wave needs to (a wave-uniform branch instead of a masked one per
-        // pair): the draws of cells that need none are discarded (qn = 1 gives thr = 0; grow is masked by EMPTY)
+        // lane): the draws of cells that need none are discarded (qn = 1 gives thr = 0; grow is masked by EMPTY)
         const bool wave_draws = __ballot(needB != 0u) != 0ull;
         // the Philox round keys are rebuilt per row by s_add (hoisted, the 20 of them were spilled to VGPR lanes
         // and read back per row)
         uint32_t rk0 = k0, rk1 = k1;
         asm volatile("" : "+s"(rk0), "+s"(rk1));
+        u32x4 X = u32x4{0u, 0u, 0u, 0u};
+        if (wave_draws) X = philox_cell(lin0 >> 2, rk0, rk1, pkc);
+        const uint32_t xw[4] = {X.x, X.y, X.z, X.w};
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            u32x4 X = u32x4{0u, 0u, 0u, 0u};
-            if (wave_draws)
-                X = philox_cell((lin0 >> 1) + (uint32_t)h, rk0, rk1);
             // thr = fl(1 - qn) * 2^24 = fl(2^24 - qn * 2^24) (power-of-two scaling commutes with the rounding)
             const gca_f2 thr = __builtin_elementwise_fma(qn[h], (gca_f2){-16777216.0f, -16777216.0f},
                                                          (gca_f2){16777216.0f, 16777216.0f});
-            const float u0 = (float)(X.x >> 8), u1 = (float)(X.z >> 8);
+            const float u0 = (float)(xw[2 * h] >> 8), u1 = (float)(xw[2 * h + 1] >> 8);
             burn |= (u0 < thr.x ? 1u : 0u) << (2 * h);
             burn |= (u1 < thr.y ? 1u : 0u) << (2 * h + 1);
             if constexpr (GROW) {
                 grow |= (u0 < pt24 ? 1u : 0u) << (2 * h);
                 grow |= (u1 < pt24 ? 1u : 0u) << (2 * h + 1);
             }
-            const uint32_t n0 = (uint32_t)randint_ms(X.y, p.age_lo, p.age_hi);
-            const uint32_t n1 = (uint32_t)randint_ms(X.w, p.age_lo, p.age_hi);
-            NA[h] = __builtin_amdgcn_perm(n1, n0, 0x05040100u);
         }
         burn &= treeB;
         grow &= emptyB;
+        {
+            const uint32_t spare = __builtin_amdgcn_perm(__builtin_amdgcn_perm(X.w, X.z, 0x0c0c0400u),
+                                                         __builtin_amdgcn_perm(X.y, X.x, 0x0c0c0400u), 0x05040100u);
+            const uint32_t n0 = (uint32_t)randint_ms(spare, p.age_lo, p.age_hi);
+            NA[0] = NA[1] = __builtin_amdgcn_perm(n0, n0, 0x05040100u);
+            // a lane with two or more new fires (dense state: ~5 % of the wave-rows): the 2nd..4th in column order
+            // take words 0..2 of the group's second block (tag ALXA)
+            if (__ballot((burn & (burn - 1u)) != 0u) != 0ull) {
+                const u32x4 Y = philox_cell(lin0 >> 2, rk0, rk1, pkc_age);
+                const uint32_t nk[4] = {n0, (uint32_t)randint_ms(Y.x, p.age_lo, p.age_hi),
+                                        (uint32_t)randint_ms(Y.y, p.age_lo, p.age_hi),
+                                        (uint32_t)randint_ms(Y.z, p.age_lo, p.age_hi)};
+                uint32_t a[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t rank = (uint32_t)__builtin_popcount(burn & ((1u << j) - 1u));
+                    a[j] = rank == 0 ? nk[0] : (rank == 1 ? nk[1] : (rank == 2 ? nk[2] : nk[3]));
+                }
+                NA[0] = __builtin_amdgcn_perm(a[1], a[0], 0x05040100u);
+                NA[1] = __builtin_amdgcn_perm(a[3], a[2], 0x05040100u);
+            }
+        }
 
         // ---- the rule on 4-bit masks: TREE -> FIRE (burn), EMPTY -> TREE (grow), FIRE -> EMPTY (age <= 1;
         //      classic: age == 1); age <= 1 <=> sat(age - 2) < 0 (saturating i16 pairs, exact for every int16)

@@ -19,6 +19,7 @@ GCA_MAX_RADIUS = 8
 
 TAG_WINDY_ROLL = 0x574E4459
 TAG_ALEX_CELL = 0x414C5843
+TAG_ALEX_AGE = 0x414C5841
 TAG_ALEX_WIND = 0x414C5857
 TAG_ACTION = 0x41435449
 TAG_INIT = 0x494E4954

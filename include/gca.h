@@ -34,7 +34,8 @@ extern "C" {
 
 /* Philox stream tags (counter word 3). */
 #define GCA_TAG_WINDY_ROLL 0x574E4459u /* 'WNDY' : 3x3 roll of WindyForestFire      */
-#define GCA_TAG_ALEX_CELL  0x414C5843u /* 'ALXC' : per-cell draws of Alexandridis    */
+#define GCA_TAG_ALEX_CELL  0x414C5843u /* 'ALXC' : per-cell draws of Alexandridis (one block per 4 cells) */
+#define GCA_TAG_ALEX_AGE   0x414C5841u /* 'ALXA' : ages of a 4-cell group's 2nd..4th new fires            */
 #define GCA_TAG_ALEX_WIND  0x414C5857u /* 'ALXW' : per-env wind change               */
 #define GCA_TAG_ACTION     0x41435449u /* 'ACTI' : synthetic actions (bench)          */
 #define GCA_TAG_INIT       0x494E4954u /* 'INIT' : synthetic initial states           */
@@ -166,7 +167,10 @@ int gca_alex_prepare_slope(const float* slope, float* p_slope, int E, int H, int
  * grid u8, fire_age i16, vegetation/density/dousing u8 (E,H,W); p_slope (E,8,H,W) f32.
  * Draws: inj_burn [E][H][W][9] f32, inj_grow [E][H][W] f32, inj_age [E][H][W] i32 (all three
  *        given = injected mode, the reference rule verbatim), or all NULL = Philox mode
- *        (one Philox4x32-10 block per cell, burn test against 1 - prod(1 - clamp01(p_d))).
+ *        (burn test against 1 - prod(1 - clamp01(p_d)); one Philox4x32-10 block per 4 cells (r, 4g .. 4g+3),
+ *        counter (r * ceil(W/4) + g, env_offset + e, rng_step[e], ALXC): cell j tests word j's high 24 bits,
+ *        the group's first new fire takes randint of the words' low bytes, its 2nd..4th words 0..2 of the
+ *        ALXA block of the same counter).
  * prob_out (nullable, debug) [E][H][W][8] f32 burn probabilities of every cell.
  * counts (nullable) [E][3] of the NEW grid, OVERWRITTEN (memset inside).          */
 int gca_alex_step(const gca_alex_params* p, int E, int H, int W, const uint8_t* grid_in, uint8_t* grid_out,

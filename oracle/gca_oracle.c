@@ -15,8 +15,11 @@
  *   p_d   = ((((p_h * av) * ad) * wind[d]) * p_slope[d])                       (:206)
  *   injected: TREE -> FIRE iff exists fire neighbour d with u[d] < p_d (:379-383)
  *   philox  : TREE -> FIRE iff u(main) < 1 - q, q = prod_{fire d} (1 - clamp01(p_d)) accumulated in d order as
- *             q = fmaf(-q, clamp01(p_d), q) (one rounding per factor), where the cell with
- *             index lin uses words (2h, 2h+1), h = lin & 1, of Philox(lin >> 1, env, step, ALXC)
+ *             q = fmaf(-q, clamp01(p_d), q) (one rounding per factor). Draws (r05): one Philox block per group of
+ *             4 cells of a row, X = Philox(r * ceil(W / 4) + (c >> 2), env, step, ALXC); cell j = c & 3 tests
+ *             main = X[j] (its high 24 bits). The group's new fires take their ages in column order: the first
+ *             from the spare word X[0].b0 | X[1].b0 << 8 | X[2].b0 << 16 | X[3].b0 << 24 (the low bytes, which
+ *             no decision reads), the k-th (k = 2..4) from word k-2 of Y = Philox(same counter, ALXA)
  *   EMPTY -> TREE iff u < p_tree; FIRE -> EMPTY iff age <= 1 (age == 1 with burnout_eq1, the
  *   classic ca_alexandridis.py:181-183); ages (:394-423). heat starts at heat0 (0, or the classic
  *   constant p_h = 0.58 of ca_alexandridis.py:94 with zero heat / dousing weights).
@@ -27,6 +30,7 @@
 #include <string.h>
 
 #define TAG_ALEX_CELL 0x414C5843u
+#define TAG_ALEX_AGE 0x414C5841u
 #define TAG_ALEX_WIND 0x414C5857u
 
 typedef struct {
@@ -148,9 +152,15 @@ static void alex_env(const oracle_alex_params* p, int e, int H, int W, const uin
             satf[i] = (g[(long)r * W + c] == p->fire) + satf[i - 1] + satf[i - (W + 1)] - satf[i - (W + 1) - 1];
             satd[i] = dous[(long)r * W + c] + satd[i - 1] + satd[i - (W + 1)] - satd[i - (W + 1) - 1];
         }
+    const uint32_t GW4 = (uint32_t)(W + 3) >> 2;
     for (int r = 0; r < H; ++r) {
+        uint32_t gX[4] = {0u, 0u, 0u, 0u};
+        int g_have = 0, g_n = 0;
+        long g_cell[4];
         for (int c = 0; c < W; ++c) {
             const long cell = (long)r * W + c;
+            const uint32_t grp = (uint32_t)r * GW4 + ((uint32_t)c >> 2);
+            if ((c & 3) == 0) g_have = g_n = 0;
             /* box sums from the summed-area tables (clamped to the grid = zero padding) */
             float ph = p->heat0, dz = 0.0f;
             const int KS = R < 2 ? 2 : R;
@@ -193,18 +203,19 @@ static void alex_env(const oracle_alex_params* p, int e, int H, int W, const uin
                 }
                 if (is_empty) grow = ig[cell] < p->p_tree;
             } else if ((is_tree && fm) || (is_empty && p->p_tree > 0.0f)) {
-                /* one Philox block per cell pair: counter lin >> 1, words (2h, 2h+1) for h = lin & 1 */
-                const uint32_t ctr[4] = {(uint32_t)cell >> 1, env_id, step, TAG_ALEX_CELL};
-                uint32_t rx[4];
-                philox(ctr, k0, k1, rx);
-                const int h = (int)(cell & 1);
-                const uint32_t main_w = rx[2 * h], aux_w = rx[2 * h + 1];
+                /* the group's block (r * ceil(W/4) + c/4, env, step, ALXC): cell j = c & 3 reads word j */
+                if (!g_have) {
+                    const uint32_t ctr[4] = {grp, env_id, step, TAG_ALEX_CELL};
+                    philox(ctr, k0, k1, gX);
+                    g_have = 1;
+                }
+                const uint32_t main_w = gX[c & 3];
                 if (is_tree) {
                     float qn = 1.0f;
                     for (int q = 0; q < 8; ++q)
                         if ((fm >> q) & 1u) qn = fmaf(-qn, clamp01(pd[q]), qn);
                     burn = u01(main_w) < 1.0f - qn;
-                    new_age = randint_ms(aux_w, p->age_lo, p->age_hi);
+                    if (burn) g_cell[g_n++] = cell; /* its age: at the end of the group, by rank */
                 } else {
                     grow = u01(main_w) < p->p_tree;
                 }
@@ -220,6 +231,19 @@ static void alex_env(const oracle_alex_params* p, int e, int H, int W, const uin
             cE += nx == p->empty;
             cT += nx == p->tree;
             cF += nx == p->fire;
+            if (g_n && ((c & 3) == 3 || c == W - 1)) {
+                /* the group's new fires in column order: the spare word of X, then words 0.. of Y (ALXA) */
+                const uint32_t spare = (gX[0] & 0xFFu) | ((gX[1] & 0xFFu) << 8) | ((gX[2] & 0xFFu) << 16) |
+                                       (gX[3] << 24);
+                uint32_t gY[4] = {0u, 0u, 0u, 0u};
+                if (g_n > 1) {
+                    const uint32_t ctr[4] = {grp, env_id, step, TAG_ALEX_AGE};
+                    philox(ctr, k0, k1, gY);
+                }
+                for (int k = 0; k < g_n; ++k)
+                    ageo[g_cell[k]] = (int16_t)randint_ms(k == 0 ? spare : gY[k - 1], p->age_lo, p->age_hi);
+                g_n = 0;
+            }
         }
     }
     free(satf);

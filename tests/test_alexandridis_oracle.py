@@ -161,3 +161,55 @@ def test_c_oracle_classic_matches_classic_restatement(H, W, seed):
     fire = ctx["grid"] == 2
     assert np.all(go[0][fire & (ctx["fire_age"] <= 0)] == 2)
     assert np.all(go[0][fire & (ctx["fire_age"] == 1)] == 0)
+
+
+def test_group_draw_convention_restated_in_numpy():
+    """The C oracle's Philox-mode draws (r05, include/gca.h GCA_TAG_ALEX_CELL / _AGE) restated in numpy from the
+    spec: group (r, c // 4) -> block X = Philox(r * ceil(W/4) + c // 4, env, step, ALXC); cell c tests word c % 4
+    (EMPTY -> TREE iff (word >> 8) < p_tree * 2^24 exactly; TREE -> FIRE iff (word >> 8) < (1 - q) * 2^24, checked
+    away from the threshold against the float64 law of the oracle's own p_d); the group's new fires in column order take
+    randint of the spare word (the four low bytes) and then of words 0, 1, 2 of Philox(same counter, ALXA). A hot state
+    at an odd width (partial last groups) so every rank occurs."""
+    from oracle.philox import philox4x32_10, randint_ms, seed_key
+
+    E, H, W, step = 2, 23, 45, 17
+    case = make_case(E, H, W, 31, fire_p=0.45, dousing_p=0.0, p_tree=0.2)
+    case["veg"][:] = 5
+    case["den"][:] = 5
+    p = params(H, 0.2)
+    ps = alex_c.prepare_slope(case["slope"])
+    go, ao, _, probs = alex_c.alex_step(p, case["grid"], case["age"], case["veg"], case["den"], case["dous"], ps,
+                                        case["widx"], rng_step=np.full(E, step, np.uint32), want_probs=True)
+    key = seed_key(p.seed)
+    GW4 = (W + 3) // 4
+    g = case["grid"]
+    pad = np.pad(g, ((0, 0), (1, 1), (1, 1)))
+    checked_burn = ranks_seen = 0
+    seen = set()
+    for e in range(E):
+        env_id = int(p.env_offset) + e
+        for r in range(H):
+            grp = r * GW4 + np.arange(GW4)
+            ctr = lambda tag: np.stack([grp, np.full(GW4, env_id), np.full(GW4, step), np.full(GW4, tag)], -1)
+            X = philox4x32_10(ctr(0x414C5843), key)
+            Y = philox4x32_10(ctr(0x414C5841), key)
+            spare = ((X[:, 0] & 0xFF) | ((X[:, 1] & 0xFF) << 8) | ((X[:, 2] & 0xFF) << 16) |
+                     ((X[:, 3] & 0xFF) << 24)).astype(np.uint32)
+            for c in range(W):
+                u24 = int(X[c // 4, c % 4]) >> 8
+                x = int(g[e, r, c])
+                if x == 0:
+                    assert (go[e, r, c] == 1) == (np.float32(u24) < np.float32(p.p_tree) * np.float32(2 ** 24))
+                elif x == 1:
+                    nb = pad[e, r:r + 3, c:c + 3].reshape(9)[[0, 1, 2, 3, 5, 6, 7, 8]] == 2
+                    law = 1.0 - np.prod(np.where(nb, 1.0 - np.clip(probs[e, r, c].astype(np.float64), 0, 1), 1.0))
+                    if abs(u24 - law * 2 ** 24) > 4:
+                        assert (go[e, r, c] == 2) == (u24 < law * 2 ** 24), (e, r, c)
+                        checked_burn += 1
+            for gi in range(GW4):
+                cols = [c for c in range(4 * gi, min(4 * gi + 4, W)) if g[e, r, c] == 1 and go[e, r, c] == 2]
+                for k, c in enumerate(cols):
+                    word = spare[gi] if k == 0 else Y[gi, k - 1]
+                    assert int(ao[e, r, c]) == int(randint_ms(np.uint32(word), p.age_lo, p.age_hi)), (e, r, c, k)
+                    seen.add(k)
+    assert checked_burn > 500 and seen == {0, 1, 2, 3}, (checked_burn, seen)
