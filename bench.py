@@ -338,8 +338,7 @@ def bench_alex(args, world, rank, device, pg):
             env.ca_step(render=fused)
         env.post_step(action, stats=True)
         if fused:
-            call("gca_obs_position", env.obs_params, E, N, N, dev.ptr(env.pos), dev.ptr(env.is_night),
-                 dev.ptr(env.time_step), dev.ptr(env.rgb), st)
+            env.finish_frame()  # the bulldozer's pixel (gca_obs_position)
         else:
             env.render_observation(None)
 
@@ -357,28 +356,40 @@ def bench_alex(args, world, rank, device, pg):
             env.rgb.fill_(0.5)
 
     _, kern_fill = timed_loop(step_fill, args.steps, args.warmup, pg, device, reps=1, prepare=prep)
-    # the extension pipeline (enable_extensions=True, extension choice 1 = unblur in every env: blur + visibility):
-    # its own observation pass (gca_adv_observation, 14 B/cell)
+    # the extension pipeline (enable_extensions=True, which also sets should_transform_grid, advanced_bulldozer.py:293-302;
+    # extension choice 1 = unblur in every env): at W = 256 the frame comes from the CA step's epilogue too
+    # (gca_alex_step_march_rgb_ext: the display is the grid while row 0 holds a TREE / FIRE, checked per env; envs whose
+    # check fails are re-rendered by gca_adv_observation with env_mask = refit), else its own pass (14 B/cell)
     from gymca_amd.forest_fire.bulldozer.observation import make_obs_params
 
-    plain_params = env.obs_params
+    plain_params, plain_ext = env.obs_params, env.enable_extensions
     env.obs_params = make_obs_params(0, 1, 2, True, True, env._day_length)
+    env.enable_extensions = True
+    fused_ext = env.fused_observation
     action3 = torch.zeros((E, 3), dtype=torch.int32, device=device)
     action3[:, 2] = 1
 
     def step_ext(events):
-        step(None)
+        call("gca_random_actions", dev.ptr(action), E, env.env_offset, 7, dev.ptr(env.rng_step), st)
         if events is not None:
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record()
+        if fused_ext:
+            env.ca_step(render=True, action=action3)
+        else:
+            env.ca_step()
+            env.post_step(action, stats=True)
             env.render_observation(action3)
+        if events is not None:
             b.record()
             events.append((a, b))
-        else:
-            env.render_observation(action3)
+        if fused_ext:
+            env.post_step(action, stats=True)
+            env.finish_frame(action3)
 
     dt_ext, kern_ext = timed_loop(step_ext, args.steps, args.warmup, pg, device, reps=3, prepare=prep)
-    env.obs_params = plain_params
+    refits = int(env._refit.sum().item()) if fused_ext else None
+    env.obs_params, env.enable_extensions = plain_params, plain_ext
     res["with_rgb_observation"] = {"env_steps_per_s": world * E * args.steps / dt_rgb,
                                    "cell_updates_per_s": world * E * N * N * args.steps / dt_rgb,
                                    "ms_per_step": dt_rgb / args.steps * 1e3,
@@ -388,12 +399,15 @@ def bench_alex(args, world, rank, device, pg):
                                    "same_buffer_fill_ms": kern_fill * 1e3,
                                    "note": "the reference's default env step (stateless_step renders RGB f32, "
                                            "enable_extensions=False): the frame from the CA step's epilogue"}
-    res["with_rgb_observation_extensions"] = {"env_steps_per_s": world * E * args.steps / dt_ext,
-                                              "ms_per_step": dt_ext / args.steps * 1e3,
-                                              "obs_kernel_ms": kern_ext * 1e3,
-                                              "obs_gbs": 14 * E * N * N / kern_ext / 1e9,
-                                              "obs_frac_of_fill": kern_fill / kern_ext,
-                                              "note": "enable_extensions=True, unblur chosen: its own pass"}
+    res["with_rgb_observation_extensions"] = {
+        "env_steps_per_s": world * E * args.steps / dt_ext,
+        "ms_per_step": dt_ext / args.steps * 1e3,
+        "fused": fused_ext,
+        ("step_and_frame_kernels_ms" if fused_ext else "step_and_separate_frame_ms"): kern_ext * 1e3,
+        "refit_envs_last_step": refits,
+        "note": ("enable_extensions=True, unblur chosen: the frame from the CA step's epilogue "
+                 "(gca_alex_step_march_rgb_ext), refit envs by gca_adv_observation after the env step" if fused_ext else
+                 "enable_extensions=True, unblur chosen: its own pass (gca_adv_observation)")}
     # the same env from its reset state (two burning cells per env, advanced_bulldozer.py:650-688): a
     # real episode's first steps, where the fire-sparsity skip leaves most waves the 7 B/cell of
     # grid/age/dousing traffic. Reported separately; the headline above is the dense mid-episode state.

@@ -40,7 +40,21 @@ struct MarchObs {
     const float4* col;     // [2 nights][3 kinds][2 dousing] colours (gca_obs_color_table)
     const int32_t* night;  // [E] pre-step is_night
     float* rgb;            // [E][H][W][3]
+    // the extension pipeline (gca_alex_step_march_rgb_ext, W = 256): per extension choice (the action's third
+    // column, clamped to [0, n_choices)) 4 bits of OBS_* below; refit[e] = 1 when env e's frame must be rendered by
+    // gca_adv_observation instead (its display needs the blur, or the speculation "row 0 of an enabled extension
+    // channel is nonzero" failed)
+    const int32_t* action;
+    int action_stride, n_choices;
+    uint32_t mode_bits;
+    uint8_t* refit;
 };
+// frame modes of an extension choice (advanced_bulldozer.py:1035-1101 with the display scan of gca_obs.hip): the
+// display is channel min(first row with a positive extension value, n_ext - 1); the kernel speculates that row 0 has
+// one, so channel 0 is shown: the grid itself (channel 0 enabled and unblurred: visibility changes only code 3, which
+// renders EMPTY either way) or zeros (channel 0 disabled); the check bits say how row 0 is tested
+constexpr uint32_t OBS_GRID = 0u, OBS_ZERO = 1u, OBS_NONE = 2u;  // bits 0-1: what the kernel renders
+constexpr uint32_t OBS_CHK_GRID = 4u, OBS_CHK_BLUR = 8u;        // speculation checks (row 0 of the new grid)
 
 // DPP across the whole wave (gfx9 wave_shr:1 / wave_shl:1); the lane without a source reads 0 (bound_ctrl: no
 // `old` operand to materialise, one v_mov_b32_dpp each)
@@ -257,6 +271,35 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
 
     if (lane < 16) lut[wl][lane] = gca_alex_lut_entry(p, lane);
     if (OBS && lane < 6) colw[wl][lane] = obs.col[6 * (obs.night[e] != 0 ? 1 : 0) + lane];
+    // the env's frame mode (OBS_*; 0 = the plain frame of the grid)
+    uint32_t omode = 0u;
+    if constexpr (OBS && !HALO) {
+        if (obs.action) {
+            const int choice = min(max(obs.action[(size_t)e * obs.action_stride + 2], 0), obs.n_choices - 1);
+            omode = (uint32_t)__builtin_amdgcn_readfirstlane((int)((obs.mode_bits >> (4 * choice)) & 0xFu));
+        }
+    }
+    // the speculation check (tile 0 of the env; values 0..2 expected, any other code in rows 0 / 1 refits): some
+    // enabled channel is positive in row 0 -- the grid (a TREE or FIRE) or its 3 x 3 edge-padded blur (round(S / 9)
+    // >= 1 <=> S >= 5, S = 2 x (row 0's three columns) + (row 1's), the f32 arithmetic of apply_blur, gca_obs.hip)
+    auto row0_refit = [&](uint32_t x0, uint32_t x1) -> uint8_t {
+        const uint32_t odd = ((x0 + 0x7D7D7D7Du) | x0 | (x1 + 0x7D7D7D7Du) | x1) & 0x80808080u;  // a byte > 2
+        bool pos = false;
+        if (omode & OBS_CHK_GRID) pos |= __ballot(x0 != 0u) != 0ull;
+        if (omode & OBS_CHK_BLUR) {
+            auto hsum = [&](uint32_t x) {  // columns c-1 + c + c+1 per byte, the grid's edge columns replicated
+                uint32_t L = __builtin_amdgcn_alignbyte(x, from_prev(x), 3);
+                uint32_t Rt = __builtin_amdgcn_alignbyte(from_next(x), x, 1);
+                if (lane == 0) L = (x << 8) | (x & 0xFFu);
+                if (lane == 63) Rt = (x >> 8) | (x & 0xFF000000u);
+                return L + x + Rt;
+            };
+            const uint32_t S = 2u * hsum(x0) + hsum(x1);
+            pos |= __ballot(((S + 0x7B7B7B7Bu) & 0x80808080u) != 0u) != 0ull;
+        }
+        const bool bad = __ballot(odd != 0u) != 0ull;
+        return ((omode & 3u) == OBS_NONE || bad || ((omode & (OBS_CHK_GRID | OBS_CHK_BLUR)) && !pos)) ? 1 : 0;
+    };
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -273,6 +316,8 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
     // then 3 x 1 KiB contiguous non-temporal stores (r03k: two rows per flush, or plain stores, measured slower)
     auto write_rgb_row = [&](int r, uint32_t tB, uint32_t fB, uint32_t dfl) {
         if constexpr (OBS) {
+            if ((omode & 3u) == OBS_NONE) return;  // rendered by gca_adv_observation (refit)
+            if ((omode & 3u) == OBS_ZERO) tB = fB = 0u;  // the display is an all-zero channel: EMPTY colours
             const uint32_t kidx = 2u * gca_spread4(tB) + 4u * gca_spread4(fB) + (dfl & 0x01010101u);
             // one cell at a time (3 live VGPRs instead of the 16 of four colours: the frame is written at the end of
             // the row, where row r+1's loads are in flight and the register file is full)
@@ -293,9 +338,14 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
 #pragma unroll
             for (int t = 0; t < 3; ++t) v[t] = img[wl][64 * t + lane];
 #pragma unroll
-            for (int t = 0; t < 3; ++t)
+            for (int t = 0; t < 3; ++t) {
+#ifdef GCA_AB_RGB_PLAIN
+                *reinterpret_cast<f4t*>(row + 4 * (64 * t + lane)) = (f4t){v[t].x, v[t].y, v[t].z, v[t].w};
+#else
                 __builtin_nontemporal_store((f4t){v[t].x, v[t].y, v[t].z, v[t].w},
                                             reinterpret_cast<f4t*>(row + 4 * (64 * t + lane)));
+#endif
+            }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // this row's reads before the next row's writes
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -326,6 +376,12 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
             cE += __builtin_popcount(bytes_eq01(gw, Ep));
             cT += __builtin_popcount(bytes_eq01(gw, Tp));
             if (OBS) write_rgb_row(r, gca_eq_nib(gw, Tp), 0u, dflags(draw_bits(r)));
+        }
+        if constexpr (OBS && !HALO) {
+            if (obs.refit && s0 == 0) {
+                const uint8_t rf = row0_refit(row(0), row(1));
+                if (lane == 0) obs.refit[e] = rf;
+            }
         }
         if (act_out && lane == 0) act_out[((size_t)e * strips + s) * NSEG + g] = 0;
         if (counts) {
@@ -511,6 +567,7 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
     const float w_in_minus_bd = __fsub_rn(p.dous_inner, p.dous_border);
     const uint32_t codes = (p.empty & 0xFFu) | ((p.tree & 0xFFu) << 8) | ((p.fire & 0xFFu) << 16);
     int cntE = 0, cntT = 0, cntF = 0;
+    uint32_t out_row0 = 0u;  // OBS refit check: the new codes of row 0 (tile 0)
 
     // one row of the tile. SC: row r's planes (0..2 as prepared own factors, 3 raw); SN: row r+1's raw planes.
     // After the row, SN holds row r+1's prepared planes and SC row r+2's raw planes (loaded once direction 4 has
@@ -909,11 +966,26 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
             nag[h] = gca_bfi32(bm, NA[h], a1);
         }
         const size_t o = (size_t)r * W + lc;
+#ifdef GCA_AB_RGB_EARLY
+        write_rgb_row(r, newT, newF, dring[3]);
+#endif
         // the new grid and ages are read back only by the next step: non-temporal stores
         __builtin_nontemporal_store(outw, reinterpret_cast<uint32_t*>(gO + o));
         { typedef uint32_t u2v __attribute__((ext_vector_type(2)));
           __builtin_nontemporal_store((u2v){nag[0], nag[1]}, reinterpret_cast<u2v*>(aO + o)); }
+#ifndef GCA_AB_RGB_EARLY
         write_rgb_row(r, newT, newF, dring[3]);
+#endif
+        if constexpr (OBS && !HALO) {
+            if (obs.refit && r < 2) {  // tile 0's rows 0 and 1 (wave-uniform)
+                if (r == 0) {
+                    out_row0 = outw;
+                } else {
+                    const uint8_t rf = row0_refit(out_row0, outw);
+                    if (lane == 0) obs.refit[e] = rf;
+                }
+            }
+        }
         cntT += __builtin_popcount(newT);
         cntF += __builtin_popcount(newF);
         cntE += __builtin_popcount(newE);
@@ -1014,6 +1086,9 @@ int march_impl(const gca_alex_params* p, int E, int H, int W, const uint8_t* gri
                     ((uintptr_t)vd) | ((uintptr_t)edge_slope) | ((uintptr_t)obs.rgb) | ((uintptr_t)obs.col)) & 15u) == 0 &&
                       ((uintptr_t)dous_bits & 1u) == 0,
                   "alex_step_march: arrays must be 16-B aligned");
+    GCA_CHECK_ARG(!obs.action || (obs.rgb && obs.refit && W == MW && obs.action_stride >= 3 && obs.n_choices >= 1 &&
+                                  p->empty == 0 && p->tree == 1 && p->fire == 2),
+                  "alex_step_march_rgb_ext: needs rgb, refit, W = 256, full actions (stride >= 3) and the codes 0 / 1 / 2");
     GCA_CHECK_ARG(!act_in || act_out, "alex_step_march: act_in needs act_out");
     GCA_CHECK_ARG(act_in != act_out || !act_in, "alex_step_march: act_in and act_out must differ");
     hipStream_t st = (hipStream_t)stream;
@@ -1032,6 +1107,34 @@ int march_impl(const gca_alex_params* p, int E, int H, int W, const uint8_t* gri
     return GCA_OK;
 }
 
+// OBS_* bits of every extension choice (see MarchObs): the display of advanced_bulldozer.py:1035-1101 under the
+// speculation that row 0 of an enabled channel is positive (then channel 0 is shown everywhere, gca_obs.hip's scan
+// stops at row 0); what needs the blurred grid, or a single channel, is left to gca_adv_observation (OBS_NONE)
+uint32_t obs_mode_bits(const gca_obs_params& op, int& n_choices) {
+    const bool ext = op.enable_extensions && op.n_choices > 0;
+    n_choices = ext ? (op.n_choices < 8 ? op.n_choices : 8) : 1;
+    uint32_t bits = 0u;
+    for (int c = 0; c < n_choices; ++c) {
+        uint32_t on = 0u;
+        if (ext)
+            for (int i = 0; i < op.n_ext && i < GCA_OBS_MAX_EXT; ++i) on |= (op.ext_lookup[c][i] != 0 ? 1u : 0u) << i;
+        uint32_t m;
+        if (!on) {
+            m = op.should_transform ? OBS_NONE : OBS_GRID;  // the base channel: blurred, or the grid
+        } else if (op.n_ext < 2) {
+            m = OBS_NONE;  // one channel: shown whenever any row is positive (not a row-0 question)
+        } else {
+            uint32_t chk = 0u;
+            for (int i = 0; i < op.n_ext && i < GCA_OBS_MAX_EXT; ++i)
+                if ((on >> i) & 1u) chk |= op.ext_skip_blur[i] ? OBS_CHK_GRID : OBS_CHK_BLUR;
+            m = (on & 1u) ? (op.ext_skip_blur[0] ? OBS_GRID : OBS_NONE) : OBS_ZERO;
+            if (m != OBS_NONE) m |= chk;
+        }
+        bits |= m << (4 * c);
+    }
+    return bits;
+}
+
 }  // namespace
 
 extern "C" int gca_alex_step_march(const gca_alex_params* p, int E, int H, int W, const uint8_t* grid_in,
@@ -1040,7 +1143,7 @@ extern "C" int gca_alex_step_march(const gca_alex_params* p, int E, int H, int W
                                    const uint32_t* rng_step, int32_t* counts, const uint8_t* act_in, uint8_t* act_out,
                                    void* stream) {
     return march_impl(p, E, H, W, grid_in, grid_out, age_in, age_out, vd, dous_bits, edge_slope, wind_index, rng_step,
-                      counts, act_in, act_out, MarchObs{nullptr, nullptr, nullptr}, stream);
+                      counts, act_in, act_out, MarchObs{nullptr, nullptr, nullptr, nullptr, 0, 1, 0u, nullptr}, stream);
 }
 
 extern "C" int gca_alex_step_march_rgb(const gca_alex_params* p, int E, int H, int W, const uint8_t* grid_in,
@@ -1052,5 +1155,24 @@ extern "C" int gca_alex_step_march_rgb(const gca_alex_params* p, int E, int H, i
     GCA_CHECK_ARG(color_table && is_night && rgb, "alex_step_march_rgb: color_table, is_night and rgb required");
     return march_impl(p, E, H, W, grid_in, grid_out, age_in, age_out, vd, dous_bits, edge_slope, wind_index, rng_step,
                       counts, act_in, act_out,
-                      MarchObs{reinterpret_cast<const float4*>(color_table), is_night, rgb}, stream);
+                      MarchObs{reinterpret_cast<const float4*>(color_table), is_night, rgb, nullptr, 0, 1, 0u, nullptr},
+                      stream);
+}
+
+extern "C" int gca_alex_step_march_rgb_ext(const gca_alex_params* p, const gca_obs_params* op, int E, int H, int W,
+                                           const uint8_t* grid_in, uint8_t* grid_out, const int16_t* age_in,
+                                           int16_t* age_out, const uint8_t* vd, const uint16_t* dous_bits,
+                                           const float* edge_slope, const int32_t* wind_index, const uint32_t* rng_step,
+                                           int32_t* counts, const uint8_t* act_in, uint8_t* act_out,
+                                           const float* color_table, const int32_t* is_night, float* rgb,
+                                           const int32_t* action, int action_stride, uint8_t* refit, void* stream) {
+    GCA_CHECK_ARG(op && color_table && is_night && rgb && action && refit,
+                  "alex_step_march_rgb_ext: obs params, color_table, is_night, rgb, action and refit required");
+    int n_choices = 1;
+    const uint32_t bits = obs_mode_bits(*op, n_choices);
+    return march_impl(p, E, H, W, grid_in, grid_out, age_in, age_out, vd, dous_bits, edge_slope, wind_index, rng_step,
+                      counts, act_in, act_out,
+                      MarchObs{reinterpret_cast<const float4*>(color_table), is_night, rgb, action, action_stride,
+                               n_choices, bits, refit},
+                      stream);
 }

@@ -201,6 +201,8 @@ _SIGNATURES = {
     "gca_alex_step_march": ([POINTER(AlexParams), c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, P, P, P], c_int),
     "gca_alex_step_march_rgb": ([POINTER(AlexParams), c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, P, P, P, P,
                                  P, P], c_int),
+    "gca_alex_step_march_rgb_ext": ([POINTER(AlexParams), POINTER(ObsParams), c_int, c_int, c_int, P, P, P, P, P, P, P,
+                                     P, P, P, P, P, P, P, P, P, c_int, P, P], c_int),
     "gca_obs_color_table": ([POINTER(ObsParams), P, P], c_int),
     "gca_obs_position": ([POINTER(ObsParams), c_int, c_int, c_int, P, P, P, P, P], c_int),
     "gca_alex_pack_layers": ([P, P, P, P, P, c_int, c_int, c_int, P], c_int),

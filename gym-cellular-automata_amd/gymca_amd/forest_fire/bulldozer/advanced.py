@@ -164,6 +164,10 @@ class AdvancedForestFireBulldozerEnv:
         # the plain observation (no extension channel, no transform: the reference's default) is written by the CA
         # step itself on the packed layout (gca_alex_step_packed_rgb) and the bulldozer's pixel by gca_obs_position;
         # extensions, other layouts and pinecones (which ignite cells after the step) render it in its own pass
+        # the extension pipeline's fused frame: envs whose display the step's epilogue cannot render (refit = 1) are
+        # rendered by gca_adv_observation after the env step (gca_alex_step_march_rgb_ext)
+        self._refit = torch.zeros(E, dtype=torch.uint8, **kw) if self.rgb is not None else None
+        self._no_ext = torch.zeros((E, 3), dtype=torch.int32, **kw) if self.rgb is not None else None
         self.obs_colors = torch.zeros((12, 4), dtype=torch.float32, **kw)
         call("gca_obs_color_table", self.obs_params, dev.ptr(self.obs_colors), dev.stream_ptr(self.device))
         self._build_context_layers(hidden_rng)
@@ -633,14 +637,26 @@ class AdvancedForestFireBulldozerEnv:
         return self.rgb
 
     @property
+    def _ext_frame(self):
+        """The extension pipeline (enable_extensions / should_transform) is rendered by the step's epilogue too: the
+        marching step at W = 256 (gca_alex_step_march_rgb_ext), with gca_adv_observation refitting the envs whose
+        display needs the blurred grid (finish_frame)."""
+        return ((self.enable_extensions or bool(self.obs_params.should_transform)) and bool(self.march)
+                and self.ncols == 256 and (self._empty, self._tree, self._fire) == (0, 1, 2))
+
+    @property
     def fused_observation(self):
         """True when env.step's RGB observation comes out of the CA step's own epilogue (see __init__)."""
-        return (self.rgb is not None and self.slope_layout == "packed" and not self.enable_extensions
-                and not self.obs_params.should_transform and not self.pinecones)
+        if self.rgb is None or self.slope_layout != "packed" or self.pinecones:
+            return False
+        plain = not self.enable_extensions and not self.obs_params.should_transform
+        return plain or self._ext_frame
 
-    def ca_step(self, render=False):
+    def ca_step(self, render=False, action=None):
         """The CA step alone (RepeatCAJax's one step) for every env; swaps the ping-pong buffers. render=True (with
-        fused_observation) also writes the step's RGB frame, all but the bulldozer's pixel."""
+        fused_observation) also writes the step's RGB frame, all but the bulldozer's pixel; with the extension
+        pipeline on, `action` holds the full actions (E, >= 3) whose third column chooses the extension, and
+        finish_frame(action) completes the frame after the env step."""
         E, H, W = self.num_envs, self.nrows, self.ncols
         a, b = self.cur, 1 - self.cur
         if self.slope_layout == "packed":
@@ -652,8 +668,14 @@ class AdvancedForestFireBulldozerEnv:
             if render:
                 if not self.fused_observation:
                     raise ValueError("ca_step(render=True) needs fused_observation")
-                call(fn + "_rgb", *args, dev.ptr(self.obs_colors), dev.ptr(self.is_night), dev.ptr(self.rgb),
-                     dev.stream_ptr(self.device))
+                if self._ext_frame:
+                    full = self._ext_action(action)
+                    call("gca_alex_step_march_rgb_ext", args[0], self.obs_params, *args[1:], dev.ptr(self.obs_colors),
+                         dev.ptr(self.is_night), dev.ptr(self.rgb), dev.ptr(full), int(full.shape[1]),
+                         dev.ptr(self._refit), dev.stream_ptr(self.device))
+                else:
+                    call(fn + "_rgb", *args, dev.ptr(self.obs_colors), dev.ptr(self.is_night), dev.ptr(self.rgb),
+                         dev.stream_ptr(self.device))
             else:
                 call(fn, *args, dev.stream_ptr(self.device))
             self._pinecones(a, b)
@@ -675,16 +697,34 @@ class AdvancedForestFireBulldozerEnv:
                  dev.ptr(self.pine_tables), dev.ptr(self.rng_step), dev.ptr(self.counts),
                  dev.ptr(None if self.act is None else self.act[b]), dev.stream_ptr(self.device))
 
+    def _ext_action(self, action):
+        """The full actions (E, >= 3) int32 device tensor the extension frame reads (no extension: choice 0)."""
+        if action is None or action.dim() != 2 or action.shape[1] < 3:
+            return self._no_ext
+        return action
+
+    def finish_frame(self, action=None):
+        """After ca_step(render=True) and post_step: the bulldozer's pixel at its new position, and (extension
+        pipeline) the frames of the envs the step's epilogue left to gca_adv_observation (refit)."""
+        E, H, W = self.num_envs, self.nrows, self.ncols
+        st = dev.stream_ptr(self.device)
+        call("gca_obs_position", self.obs_params, E, H, W, dev.ptr(self.pos), dev.ptr(self.is_night),
+             dev.ptr(self.time_step), dev.ptr(self.rgb), st)
+        if self._ext_frame:
+            full = self._ext_action(action)
+            call("gca_adv_observation", self.obs_params, 0, E, H, W, dev.ptr(self.grid[self.cur]), dev.ptr(self.dousing),
+                 dev.ptr(self.pos), dev.ptr(self.is_night), dev.ptr(self.time_step), dev.ptr(full),
+                 int(full.shape[1]), dev.ptr(self.rgb), None, dev.ptr(self._refit), st)
+
     def step(self, action):
         """Gymnasium-style step of every env: action (E, 2) or (E, 3) ints (move, shoot[, extension choice]),
         device tensor or numpy. Returns (obs, reward, terminated, truncated, info) like stateless_step."""
         full = self._full_action(action)
         fused = self.fused_observation
-        self.ca_step(render=fused)
+        self.ca_step(render=fused, action=full)
         self.post_step(full[:, :2].contiguous(), stats=True)
-        if fused:  # the frame came with the CA step; the bulldozer's pixel at its new position
-            call("gca_obs_position", self.obs_params, self.num_envs, self.nrows, self.ncols, dev.ptr(self.pos),
-                 dev.ptr(self.is_night), dev.ptr(self.time_step), dev.ptr(self.rgb), dev.stream_ptr(self.device))
+        if fused:  # the frame came with the CA step; the bulldozer's pixel at its new position (+ refits)
+            self.finish_frame(full)
         elif self.rgb is not None:
             self.render_observation(full)
         return self._obs(), self.reward, self.done.bool(), self.truncated, self._info()

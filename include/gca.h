@@ -416,6 +416,22 @@ int gca_adv_observation(const gca_obs_params* p, int mode, int E, int H, int W, 
                         const int32_t* action, int action_stride, float* rgb, uint8_t* channels,
                         const uint8_t* env_mask, void* stream);
 
+/* gca_alex_step_march_rgb for the extension pipeline (W = 256, codes 0 / 1 / 2): the frame of gca_adv_observation
+ * mode 0 (action = the full actions, action_stride >= 3) from the CA step's epilogue, minus the bulldozer's pixel
+ * (gca_obs_position), for every env whose display is channel 0 of the extended grid -- the grid itself (the unblur
+ * choice) or all zeros (see_invisible_fires: its blur is shown only when row 0 of the blur is empty; the reference's
+ * row-vs-channel display scan, advanced_bulldozer.py:1035-1064). The kernel checks that speculation on row 0 of the
+ * new grid and sets refit[e] = 1 (else 0) when it fails or when the display needs the blurred grid (no extension
+ * chosen with should_transform): those envs' frames are left for gca_adv_observation with env_mask = refit, after
+ * the env step. Results of the pair are bit for bit gca_adv_observation's. */
+int gca_alex_step_march_rgb_ext(const gca_alex_params* p, const gca_obs_params* op, int E, int H, int W,
+                                const uint8_t* grid_in, uint8_t* grid_out, const int16_t* age_in, int16_t* age_out,
+                                const uint8_t* vd, const uint16_t* dous_bits, const float* edge_slope,
+                                const int32_t* wind_index, const uint32_t* rng_step, int32_t* counts,
+                                const uint8_t* act_in, uint8_t* act_out, const float* color_table,
+                                const int32_t* is_night, float* rgb, const int32_t* action, int action_stride,
+                                uint8_t* refit, void* stream);
+
 /* [night][kind empty / tree / fire][dousing 0 / 1] float4 colours (rgb, 0) of grid_to_rgb (advanced_bulldozer.py:1041-1093),
  * the table gca_alex_step_packed_rgb reads: table[12][4] f32 device, 16-B aligned. */
 int gca_obs_color_table(const gca_obs_params* p, float* table, void* stream);

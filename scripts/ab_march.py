@@ -67,11 +67,11 @@ def main(E=4096, N=256, K=10, reps=5, hidden=False, only=None, rgb_modes=(False,
 
 if __name__ == "__main__":
     # --only march|packed: one mapping; --plain: no fused-frame variants; --reps N; --size N (grid side), --envs E;
-    # --reset: time from the reset state instead of the bench's mid-episode state
+    # --reset: time from the reset state instead of the bench's mid-episode state; --rgb-only: the fused-frame variants
     args = sys.argv[1:]
     only = args[args.index("--only") + 1] if "--only" in args else None
     reps = int(args[args.index("--reps") + 1]) if "--reps" in args else 5
     N = int(args[args.index("--size") + 1]) if "--size" in args else 256
     E = int(args[args.index("--envs") + 1]) if "--envs" in args else 4096
     main(E=E, N=N, hidden="--hidden" in args, only=only, reps=reps,
-         rgb_modes=(False,) if "--plain" in args else (False, True), reset_state="--reset" in args)
+         rgb_modes=(False,) if "--plain" in args else ((True,) if "--rgb-only" in args else (False, True)), reset_state="--reset" in args)

@@ -145,3 +145,53 @@ def test_fused_step_observation_matches_reference(device, tile_skip, W):
             env.done[1] = 1
             env.conditional_reset()
     assert int(env.dousing.sum()) > 0 and env.is_night.cpu().numpy().any()
+
+
+@pytest.mark.parametrize("tile_skip", [False, True])
+def test_fused_extension_frame_matches_reference(device, tile_skip):
+    """the extension pipeline's frame (enable_extensions=True, should_transform with it) from the
+    marching step's epilogue (gca_alex_step_march_rgb_ext, W = 256) + the bulldozer's pixel + the refit pass of
+    gca_adv_observation for the envs whose display the epilogue cannot give (no extension chosen: the blurred grid;
+    row 0 of the chosen channel empty: the reference's row-vs-channel display scan) equals the literal restatement of
+    build_observation_on_extensions / grid_to_rgb_with_extensions (advanced_bulldozer.py:988-1101,
+    extension_utils.py:89-134) for every extension choice, on envs whose first rows are burnt out (speculation fails),
+    an all-empty env, and through a day / night toggle and a conditional reset."""
+    import torch
+
+    from gymca_amd.forest_fire.bulldozer import AdvancedForestFireBulldozerEnv
+    from gymca_amd.forest_fire.bulldozer.observation import EXTENSION_LOOKUP
+
+    E, N = 9, 256
+    env = AdvancedForestFireBulldozerEnv(N, N, key=12, num_envs=E, use_hidden=True, device=device, observation="rgb",
+                                         hidden_rng="philox", enable_extensions=True, tile_skip=tile_skip)
+    assert env.march and env._ext_frame and env.fused_observation
+    env.reset()
+    g = env.grid[env.cur].clone()
+    g[3, :2] = 0   # row 0 empty (and row 1): the unblur channel's row 0 is empty -> refit
+    g[4, :1] = 0   # row 0 empty only
+    g[5] = 0       # no TREE / FIRE at all -> the base channel
+    g[6, :1, :] = 1  # a full TREE row 0: the blur of row 0 is positive
+    rng = np.random.default_rng(5)
+    g[7] = torch.as_tensor(rng.choice([0, 1, 2], size=(N, N), p=[0.3, 0.5, 0.2]).astype(np.uint8), device=device)
+    env.set_state(grid=g)
+    env.pos[:, 0], env.pos[:, 1] = 190, 60
+    env.time_step.fill_(397)
+    refit_seen = set()
+    for s in range(7):
+        night_pre = env.is_night.cpu().numpy().copy()
+        dous_pre = env.dousing.cpu().numpy().astype(np.int32)
+        act = np.stack([rng.integers(0, 9, E), rng.integers(0, 2, E), (np.arange(E) + s) % 3], axis=1)
+        (rgb, _), _, _, _, _ = env.step(torch.as_tensor(act, device=device))
+        refit_seen |= {int(x) for x in env._refit.cpu().numpy()}
+        gn = env.grid[env.cur].cpu().numpy()
+        pos = env.pos.cpu().numpy()
+        rgb = rgb.cpu().numpy()
+        for e in range(E):
+            want, _ = ob.step_observation(gn[e].astype(np.int32), tuple(pos[e]), EXTENSION_LOOKUP[act[e, 2]],
+                                          int(night_pre[e]), dous_pre[e], True, True)
+            assert np.array_equal(rgb[e], want), (s, e, int(act[e, 2]), int(env._refit[e]))
+        if s == 3:
+            env.done[2] = 1
+            env.conditional_reset()
+    assert refit_seen == {0, 1}
+    assert env.is_night.cpu().numpy().any()
