@@ -9,6 +9,7 @@ from every rank: done flags and episode returns / lengths (reference analogue: t
 disabled jax.lax.all_gather of EpisodeStatistics, agents/jax_ppo.py:1325-1348).
 Messages are ~9 KB per rank per env step: latency-bound, one all_gather per call.
 """
+import weakref
 import torch
 import torch.distributed as dist
 
@@ -90,7 +91,9 @@ class StatsGather:
     def __init__(self, num_envs, device, group=None, buffers=2, len_dtype=torch.int32, world=None, collective=None):
         self.E = int(num_envs)
         self.device = torch.device(device)
-        self.group = group
+        # an explicit group is held weakly (torch keeps it alive until destroy_process_group): a cached gather must
+        # not keep a destroyed group and its buffers alive (all_gather_stats)
+        self._group = None if group is None else weakref.ref(group)
         self.buffers = int(buffers)
         self.len_dtype = len_dtype
         self._world_override = None if world is None else int(world)
@@ -101,6 +104,15 @@ class StatsGather:
         self.world = None
         self.stream = None
         self._build(*self._world_now())
+
+    @property
+    def group(self):
+        if self._group is None:
+            return None
+        g = self._group()
+        if g is None:
+            raise RuntimeError("StatsGather: its process group has been destroyed")
+        return g
 
     def _world_now(self):
         if self._world_override is not None:
@@ -170,7 +182,11 @@ class StatsGather:
         return (d, r, ln, event) if async_op else (d, r, ln)
 
 
+# cached StatsGathers: the default group's by (E, device); an explicit group's in a dict held WEAKLY by the group
+# object (keying a plain dict by the group kept every destroyed group and its [world, row] device buffers
+# alive across init / destroy cycles)
 _GATHERS = {}
+_GROUP_GATHERS = weakref.WeakKeyDictionary()
 
 
 def all_gather_stats(done, ret, length, group=None):
@@ -178,8 +194,9 @@ def all_gather_stats(done, ret, length, group=None):
     (9 bytes per env on the wire), through a StatsGather kept per (E, device, group) — the collective allocates
     nothing; the results are fresh clones (the hot path that wants the reused views calls StatsGather directly).
     The StatsGather re-reads the world size on every call, so a cached one follows a re-initialised group."""
-    key = (done.numel(), str(done.device), group)  # the group object itself: its id could be reused once freed
-    g = _GATHERS.get(key)
+    cache = _GATHERS if group is None else _GROUP_GATHERS.setdefault(group, {})
+    key = (done.numel(), str(done.device))
+    g = cache.get(key)
     if g is None:
-        g = _GATHERS[key] = StatsGather(done.numel(), done.device, group=group, len_dtype=length.dtype)
+        g = cache[key] = StatsGather(done.numel(), done.device, group=group, len_dtype=length.dtype)
     return tuple(x.clone() for x in g.gather(done, ret, length))

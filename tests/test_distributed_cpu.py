@@ -192,3 +192,48 @@ def test_bench_torchrun_launch_measures_the_cpu_baseline_on_rank0():
 def test_bench_refuses_a_world_size_mismatch():
     rc, out, err = _bench("--gpus", "2", env={"WORLD_SIZE": "1", "RANK": "0"})
     assert rc != 0 and out is None and "WORLD_SIZE=1" in err
+
+
+def _group_gather_worker(rank, world, port, q):
+    import gc
+    import weakref
+
+    import torch
+    import torch.distributed as dist
+
+    from gymca_amd import distributed as gd
+
+    try:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        refs = []
+        for cycle in range(3):
+            g = dist.new_group([0, 1])
+            d, r, ln = gd.all_gather_stats(torch.tensor([1, 0], dtype=torch.uint8), torch.tensor([0.5, -1.0]),
+                                           torch.tensor([3, 4], dtype=torch.int32), group=g)
+            assert d.shape == (2, 2) and float(r[1, 1]) == -1.0
+            refs.append(weakref.ref(g))
+            dist.destroy_process_group(g)
+            del g
+        gc.collect()
+        alive = sum(ref() is not None for ref in refs)
+        q.put((rank, alive, len(gd._GROUP_GATHERS)))
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        q.put((rank, repr(e), None))
+
+
+def test_all_gather_stats_does_not_keep_destroyed_groups():
+    """all_gather_stats caches a StatsGather per explicit group; after destroy_process_group(g) neither the
+    group nor its cached gather stays alive (three create / gather / destroy cycles, gloo world 2)."""
+    import multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_group_gather_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    assert res == [(0, 0, 0), (1, 0, 0)], res

@@ -195,3 +195,44 @@ def test_fused_extension_frame_matches_reference(device, tile_skip):
             env.conditional_reset()
     assert refit_seen == {0, 1}
     assert env.is_night.cpu().numpy().any()
+
+
+@pytest.mark.parametrize("enable", [False, True])
+def test_fused_frames_equal_the_observation_pass_at_config3(device, enable):
+    """BASELINE config 3's full batch (4096 x 256^2, the bench's mid-episode state): the frame the marching step writes
+    in its epilogue (plain: gca_alex_step_march_rgb; extension pipeline: gca_alex_step_march_rgb_ext with the three
+    extension choices spread over the envs, some envs' first rows burnt out, + the refit pass) equals, on every env,
+    the frame gca_adv_observation renders from the same post-step state (the pass the oracle tests pin)."""
+    import torch
+
+    from gymca_amd import _device as dev
+    from gymca_amd._lib import call
+    from gymca_amd.forest_fire.bulldozer import AdvancedForestFireBulldozerEnv
+
+    E, N = 4096, 256
+    env = AdvancedForestFireBulldozerEnv(N, N, key=1, num_envs=E, use_hidden=False, device=device, observation="rgb",
+                                         enable_extensions=enable)
+    assert env.fused_observation
+    env.reset()
+    gen = torch.Generator(device=device).manual_seed(77)
+    u = torch.rand((E, N, N), device=device, generator=gen)
+    g = torch.where(u < 0.1, 0, torch.where(u < 0.9, 1, 2)).to(torch.uint8)
+    g[::97, :2] = 0  # rows 0-1 burnt out in some envs (the extension frame's row-0 speculation fails there)
+    age = torch.where(g == 2, torch.randint(1, 673, (E, N, N), device=device, generator=gen, dtype=torch.int16),
+                      torch.zeros((), dtype=torch.int16, device=device))
+    env.set_state(grid=g, fire_age=age, wind_index=torch.randint(0, 8, (E,), device=device, generator=gen,
+                                                                  dtype=torch.int32))
+    del u, g, age
+    action = torch.stack([torch.randint(0, 9, (E,), device=device, generator=gen),
+                          torch.randint(0, 2, (E,), device=device, generator=gen),
+                          torch.arange(E, device=device) % 3], 1).to(torch.int32).contiguous()
+    want = torch.empty_like(env.rgb)
+    for s in range(2):
+        env.step(action)
+        call("gca_adv_observation", env.obs_params, 0, E, N, N, dev.ptr(env.grid[env.cur]), dev.ptr(env.dousing),
+             dev.ptr(env.pos), dev.ptr(env.is_night), dev.ptr(env.time_step), dev.ptr(action), 3, dev.ptr(want), None,
+             None, dev.stream_ptr(device))
+        diff = (env.rgb != want).reshape(E, -1).any(-1)
+        assert not bool(diff.any()), (s, torch.nonzero(diff)[:5].flatten().tolist())
+    if enable:
+        assert 0 < int(env._refit.sum()) < E  # both the epilogue's frames and refits
