@@ -580,13 +580,23 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
         const uint2 agep = nAge;
         {  // (wave-uniform row base pointers + a 32-bit lane byte offset; raw buffer loads with SGPR row offsets were
            //  measured 2.5 % slower, profiles/r03n/ab_buffer_loads.txt)
+            // the tile's last row loads nothing it uses (row r+1 is the next tile's): its five loads read row 0 of env 0
+            // instead, one block every wave shares (L2-resident; r05: ~0.2 B / cell of HBM traffic, the ages and
+            // vegetation-density rows being non-temporal streams)
+            const bool ahead = i + 1 < SH;
             const int rg = r + 1 + R, rd = r + 3;
             const uint32_t r1 = (uint32_t)min(r + 1, H - 1);
-            const uint32_t gl = ld_at<uint32_t>(gE + (size_t)min(rg, H - 1) * W, lc);
-            const uint32_t d = ld_at<uint16_t>(dE + (size_t)min(rd, H - 1) * (W / 16), lane_d);
-            nOwn = ld_at<uint32_t>(gE + (size_t)r1 * W, lc);
-            nVD = ld_nt<uint32_t>(vE + (size_t)r1 * W, lc);
-            nAge = ld_nt<uint2>(aE + (size_t)r1 * W, lane_a);
+            const uint8_t* gB = ahead ? gE : grid_in;
+            const uint16_t* dB = ahead ? dE : dbits;
+            const uint8_t* vB = ahead ? vE : vd;
+            const int16_t* aB = ahead ? aE : age_in;
+            const uint32_t rgo = ahead ? (uint32_t)min(rg, H - 1) : 0u, rdo = ahead ? (uint32_t)min(rd, H - 1) : 0u;
+            const uint32_t r1o = ahead ? r1 : 0u;
+            const uint32_t gl = ld_at<uint32_t>(gB + (size_t)rgo * W, lc);
+            const uint32_t d = ld_at<uint16_t>(dB + (size_t)rdo * (W / 16), lane_d);
+            nOwn = ld_at<uint32_t>(gB + (size_t)r1o * W, lc);
+            nVD = ld_nt<uint32_t>(vB + (size_t)r1o * W, lc);
+            nAge = ld_nt<uint2>(aB + (size_t)r1o * W, lane_a);
             nG = rg < H ? gl : Ep;
             nD = rd < H ? d : 0u;
         }

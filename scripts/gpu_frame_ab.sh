@@ -11,9 +11,9 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-me
 RC=$?; echo "pytest exit $RC" >> $O/pytest_gpu.log
 [ $RC -eq 0 ] || [ $RC -eq 1 ] || exit 20
 for pass in 1 2 3; do
-  echo "pass $pass main $(timeout -k 10 180 python3 -u scripts/ab_march.py --only march --rgb-only --reps 5)" >> $O/ab.txt || exit 21
+  echo "pass $pass main $(timeout -k 10 180 python3 -u scripts/ab_march.py --only march ${AB_ARGS:---rgb-only} --reps 5)" >> $O/ab.txt || exit 21
   for v in $VARS; do
-    echo "pass $pass $v $(GCA_LIB_PATH=$V/$v.so timeout -k 10 180 python3 -u scripts/ab_march.py --only march --rgb-only --reps 5)" >> $O/ab.txt || exit 22
+    echo "pass $pass $v $(GCA_LIB_PATH=$V/$v.so timeout -k 10 180 python3 -u scripts/ab_march.py --only march ${AB_ARGS:---rgb-only} --reps 5)" >> $O/ab.txt || exit 22
   done
 done
 P=$O/prof_rgb
