@@ -242,6 +242,8 @@ def load():
         )
     lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_LOCAL)
     for name, (argtypes, restype) in _SIGNATURES.items():
+        if os.environ.get("GCA_LIB_PATH") and not hasattr(lib, name):
+            continue  # an A/B build of an older tree may predate an entry point
         fn = getattr(lib, name)
         fn.argtypes = argtypes
         fn.restype = restype
