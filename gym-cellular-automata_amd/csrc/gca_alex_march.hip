@@ -337,15 +337,11 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
             float4 v[3];
 #pragma unroll
             for (int t = 0; t < 3; ++t) v[t] = img[wl][64 * t + lane];
+            // (r05 A/B, profiles/r05c/ab.txt: plain stores +4 %; the frame written before the grid / age stores: equal)
 #pragma unroll
-            for (int t = 0; t < 3; ++t) {
-#ifdef GCA_AB_RGB_PLAIN
-                *reinterpret_cast<f4t*>(row + 4 * (64 * t + lane)) = (f4t){v[t].x, v[t].y, v[t].z, v[t].w};
-#else
+            for (int t = 0; t < 3; ++t)
                 __builtin_nontemporal_store((f4t){v[t].x, v[t].y, v[t].z, v[t].w},
                                             reinterpret_cast<f4t*>(row + 4 * (64 * t + lane)));
-#endif
-            }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // this row's reads before the next row's writes
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -580,23 +576,16 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
         const uint2 agep = nAge;
         {  // (wave-uniform row base pointers + a 32-bit lane byte offset; raw buffer loads with SGPR row offsets were
            //  measured 2.5 % slower, profiles/r03n/ab_buffer_loads.txt)
-            // the tile's last row loads nothing it uses (row r+1 is the next tile's): its five loads read row 0 of env 0
-            // instead, one block every wave shares (L2-resident; r05: ~0.2 B / cell of HBM traffic, the ages and
-            // vegetation-density rows being non-temporal streams)
-            const bool ahead = i + 1 < SH;
+            // (the tile's last row loads the next tile's row r+1 here, unused; reading one shared row instead -- ~0.2
+            //  B / cell less HBM traffic -- measured 1 % slower, profiles/r05c/ab.txt: ~3000 waves on the same
+            //  few hundred bytes)
             const int rg = r + 1 + R, rd = r + 3;
             const uint32_t r1 = (uint32_t)min(r + 1, H - 1);
-            const uint8_t* gB = ahead ? gE : grid_in;
-            const uint16_t* dB = ahead ? dE : dbits;
-            const uint8_t* vB = ahead ? vE : vd;
-            const int16_t* aB = ahead ? aE : age_in;
-            const uint32_t rgo = ahead ? (uint32_t)min(rg, H - 1) : 0u, rdo = ahead ? (uint32_t)min(rd, H - 1) : 0u;
-            const uint32_t r1o = ahead ? r1 : 0u;
-            const uint32_t gl = ld_at<uint32_t>(gB + (size_t)rgo * W, lc);
-            const uint32_t d = ld_at<uint16_t>(dB + (size_t)rdo * (W / 16), lane_d);
-            nOwn = ld_at<uint32_t>(gB + (size_t)r1o * W, lc);
-            nVD = ld_nt<uint32_t>(vB + (size_t)r1o * W, lc);
-            nAge = ld_nt<uint2>(aB + (size_t)r1o * W, lane_a);
+            const uint32_t gl = ld_at<uint32_t>(gE + (size_t)min(rg, H - 1) * W, lc);
+            const uint32_t d = ld_at<uint16_t>(dE + (size_t)min(rd, H - 1) * (W / 16), lane_d);
+            nOwn = ld_at<uint32_t>(gE + (size_t)r1 * W, lc);
+            nVD = ld_nt<uint32_t>(vE + (size_t)r1 * W, lc);
+            nAge = ld_nt<uint2>(aE + (size_t)r1 * W, lane_a);
             nG = rg < H ? gl : Ep;
             nD = rd < H ? d : 0u;
         }
@@ -976,16 +965,11 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
             nag[h] = gca_bfi32(bm, NA[h], a1);
         }
         const size_t o = (size_t)r * W + lc;
-#ifdef GCA_AB_RGB_EARLY
-        write_rgb_row(r, newT, newF, dring[3]);
-#endif
         // the new grid and ages are read back only by the next step: non-temporal stores
         __builtin_nontemporal_store(outw, reinterpret_cast<uint32_t*>(gO + o));
         { typedef uint32_t u2v __attribute__((ext_vector_type(2)));
           __builtin_nontemporal_store((u2v){nag[0], nag[1]}, reinterpret_cast<u2v*>(aO + o)); }
-#ifndef GCA_AB_RGB_EARLY
         write_rgb_row(r, newT, newF, dring[3]);
-#endif
         if constexpr (OBS && !HALO) {
             if (obs.refit && r < 2) {  // tile 0's rows 0 and 1 (wave-uniform)
                 if (r == 0) {

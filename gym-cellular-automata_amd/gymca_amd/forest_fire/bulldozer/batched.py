@@ -160,6 +160,13 @@ class BatchedForestFireBulldozerEnv:
         self._act_buf.copy_(src.reshape(E, 2))
         return self._act_buf
 
+    def rebind(self):
+        """Drop the pre-bound step call. The env's state tensors (buf, accu, steps, done, wind, rng_step, parity, pos,
+        counts, hit, reward, steps_elapsed) and params are bound by address on the first fused step; every method here
+        updates them in place. Code that REPLACES one of them (assigns a new tensor) calls rebind() afterwards."""
+        self._fused_call = self._bound_meet = None
+        self._sample_call = None
+
     def _bind_fused(self):
         E, H, W = self.num_envs, self.nrows, self.ncols
         meet = self._meet
