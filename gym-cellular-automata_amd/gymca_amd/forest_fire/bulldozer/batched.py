@@ -164,8 +164,13 @@ class BatchedForestFireBulldozerEnv:
         """Drop the pre-bound step call. The env's state tensors (buf, accu, steps, done, wind, rng_step, parity, pos,
         counts, hit, reward, steps_elapsed) and params are bound by address on the first fused step; every method here
         updates them in place. Code that REPLACES one of them (assigns a new tensor) calls rebind() afterwards."""
+        import torch
+
         self._fused_call = self._bound_meet = None
         self._sample_call = None
+        self._done_bool = self.done.view(torch.bool)
+        self._info = {"hit": self.hit, "ca_steps": self.steps}
+        self._ctx = {"wind": self.wind, "position": self.pos, "time": self.accu}
 
     def _bind_fused(self):
         E, H, W = self.num_envs, self.nrows, self.ncols

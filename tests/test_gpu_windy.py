@@ -497,3 +497,28 @@ def test_eager_step_action_forms_and_sampler(device):
             assert torch.equal(env.grids(), envs[0].grids()), f"step {s}"
             for name in ("pos", "accu", "counts", "rng_step", "hit", "done"):
                 assert torch.equal(getattr(env, name), getattr(envs[0], name)), f"{name} step {s}"
+
+
+def test_rebind_after_replacing_a_state_tensor(device):
+    """The fused step's pre-bound call holds the state tensors by address; an env whose tensor is REPLACED (not updated
+    in place) and then rebind()-ed steps exactly like an env that never had it replaced."""
+    import torch
+
+    from gymca_amd.forest_fire.bulldozer import BatchedForestFireBulldozerEnv
+
+    E, N = 32, 256
+    envs = [BatchedForestFireBulldozerEnv(E, N, N, device=device, seed=13, materialize_obs=False) for _ in range(2)]
+    acts = [torch.zeros((E, 2), dtype=torch.int32, device=device) for _ in envs]
+    for env in envs:
+        env.reset(seed=1)
+    for s in range(30):
+        if s == 10:  # replace the accumulators and the counts of env 1 by copies, then rebind
+            envs[1].accu = envs[1].accu.clone()
+            envs[1].counts = envs[1].counts.clone()
+            envs[1].rebind()
+        for env, a in zip(envs, acts):
+            env.step(env.sample_actions(a, 3))
+        assert torch.equal(envs[0].grids(), envs[1].grids()), s
+        for name in ("accu", "counts", "pos", "rng_step", "done"):
+            assert torch.equal(getattr(envs[0], name), getattr(envs[1], name)), (name, s)
+    assert envs[1]._ctx["time"] is envs[1].accu
