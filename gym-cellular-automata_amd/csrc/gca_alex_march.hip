@@ -212,7 +212,10 @@ constexpr int XI = 16;
 constexpr int XS_ONE = 13, XS_TWO = 14;  // items holding raw slopes (1.0 in the border slots: factor 1)
 
 template <int R, bool OBS, bool GROW, int NSEG>  // GROW: p_tree > 0 (EMPTY cells draw too); W = 256 * NSEG
-__global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_waves_per_eu(3, 3))) void alex_march_kernel(
+// occupancy: 3 waves / SIMD for the step (VGPR-bound, <= 168; 4 would spill), 2 for the fused frame: its 3 KiB per
+// wave-row of f32 RGB stores run faster from fewer concurrent waves (r05g, same box: 1.760 -> 1.723 ms per 4096 x 256^2
+// step with the frame; the plain step at 2 waves: +8 %)
+__global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_waves_per_eu(OBS ? 2 : 3, OBS ? 2 : 3))) void alex_march_kernel(
     gca_alex_params p, int H, int nwaves, const uint8_t* __restrict__ grid_in, uint8_t* __restrict__ grid_out,
     const int16_t* age_in, int16_t* age_out,  // no __restrict__: the env updates ages in place
     const uint8_t* __restrict__ vd, const uint16_t* __restrict__ dbits, const float* __restrict__ es,
