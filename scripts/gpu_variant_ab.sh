@@ -9,7 +9,7 @@ V=$R/gym-cellular-automata_amd/gymca_amd/_lib/variants
 O=$R/gpurun_out/$TAG
 mkdir -p $O
 for v in $VARS; do
-  GCA_LIB_PATH=$V/$v.so timeout -k 10 300 python -u -m pytest tests/test_gpu_alex_march.py tests/test_gpu_alex_draws.py -m gpu -q --timeout 200 --timeout-method thread -p no:cacheprovider > $O/pytest_$v.log 2>&1
+  GCA_LIB_PATH=$V/$v.so timeout -k 10 300 python -u -m pytest tests/test_gpu_alex_march.py tests/test_gpu_alex_draws.py tests/test_gpu_observation.py -m gpu -q --timeout 200 --timeout-method thread -p no:cacheprovider > $O/pytest_$v.log 2>&1
   RC=$?; echo "pytest exit $RC" >> $O/pytest_$v.log
   [ $RC -eq 0 ] || [ $RC -eq 1 ] || exit 20
 done
