@@ -495,6 +495,9 @@ def bench_windy(args, world, rank, device, pg):
     Kg = max(K // G, 5)
     restore = env_snapshot(env, one_step, 64)
     dt_eager, _ = timed_loop(lambda ev: one_step(), Kg * G, 0, pg, device, reps=3, prepare=restore)
+    # the same steps with the random policy's draw inside the env step (gca_bulldozer_step_fused_random: the same
+    # actions bit for bit, one launch per env step instead of two)
+    dt_rand, _ = timed_loop(lambda ev: env.step_random(9, action), Kg * G, 0, pg, device, reps=3, prepare=restore)
     # the same steps replayed from one HIP graph per G env steps (no host launch overhead)
     graph = StepGraph(one_step, n_steps=G, device=device)
     dt_env, _ = timed_loop(lambda ev: graph.replay(), Kg, 0, pg, device, reps=3, prepare=restore)
@@ -537,8 +540,9 @@ def bench_windy(args, world, rank, device, pg):
         "config": "ForestFireBulldozer 256x256, 1024 envs/GPU, WindyForestFire",
         "env_steps_per_s": world * E * Kg * G / dt_env,
         "env_steps_per_s_eager": world * E * Kg * G / dt_eager,
-        "loops": f"eager and graph: the same {Kg * G} env steps from one mid-episode state (reset + 64 steps, restored "
-                 f"before each repetition), median of 3",
+        "env_steps_per_s_random_policy_fused": world * E * Kg * G / dt_rand,
+        "loops": f"eager, graph and random-policy-fused: the same {Kg * G} env steps from one mid-episode state (reset + "
+                 f"64 steps, restored before each repetition), median of 3",
         "env_step_graph": f"hipGraph of {G} env steps (random actions + " + (
             "gca_bulldozer_step_fused: RepeatCA, Windy CA, Move/Modify and reward in one launch)" if env.fused else
             "RepeatCA/Windy passes + Move/Modify + reward)"),
@@ -590,9 +594,14 @@ def bench_windy512(args, world, rank, device, pg):
         one_step()
         gather(async_op=True)
 
+    def random_fused(ev):
+        env.step_random(11, action)
+        gather()
+
     restore = env_snapshot(env, one_step, 64)
     dt_eager, _ = timed_loop(eager, K, 0, pg, device, reps=3, prepare=restore)
     dt_async, _ = timed_loop(overlapped, K, 0, pg, device, reps=3, prepare=restore)
+    dt_rand, _ = timed_loop(random_fused, K, 0, pg, device, reps=3, prepare=restore)
     graph = StepGraph(one_step, n_steps=G, device=device)
 
     def seg(ev):
@@ -609,6 +618,7 @@ def bench_windy512(args, world, rank, device, pg):
                          "pre / Windy passes / post kernels"),
             "env_steps_per_s_eager_gather_every_step": world * E * K / dt_eager,
             "env_steps_per_s_async_gather_every_step": world * E * K / dt_async,
+            "env_steps_per_s_random_policy_fused_gather_every_step": world * E * K / dt_rand,
             "loops": f"graph / eager / async: the same {K} env steps from one mid-episode state (reset + 64 steps, "
                      f"restored before each repetition), median of 3",
             "gather": ("RCCL all_gather_into_tensor of reward f32 | length | done u8 per env into a reused buffer "

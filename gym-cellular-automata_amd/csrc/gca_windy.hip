@@ -481,25 +481,50 @@ template <int NW> constexpr int FUSED_RD = NW == 1 ? 16 : 8;
 // accu, then the wind, after the CA the position, the counts ... measured 13.6 us per 1024 x 256^2 env step with
 // the loads where they are used, r03u). A launch of fewer, resident workgroups looping over the envs measured
 // slower still (16.3 us, r03v: each workgroup then pays its envs' chains one after the other).
+// The env's action: the caller's (action != NULL), or -- gca_bulldozer_step_fused_random, a random policy -- drawn here
+// exactly as gca_random_actions draws it (Philox (0, global env id, rng_step[e], ACTI) under the policy's seed: move =
+// randint[0, 9), shoot = top bit of word 1), and written to pol.out when given.
+struct FusedPolicy {
+    uint64_t seed;
+    int32_t* out;
+};
+__device__ __forceinline__ void fused_action(const int32_t* __restrict__ action, const FusedPolicy& pol, int e,
+                                             uint32_t env_id, uint32_t rs, int32_t& a0, int32_t& a1) {
+    if (action) {
+        a0 = action[2 * e];
+        a1 = action[2 * e + 1];
+    } else {
+        const u32x4 x = philox4x32_10(u32x4{0u, env_id, rs, GCA_TAG_ACTION}, (uint32_t)pol.seed,
+                                      (uint32_t)(pol.seed >> 32));
+        a0 = randint_ms(x.x, 0, 9);
+        a1 = (int32_t)(x.y >> 31);
+    }
+}
+
 template <int NW, bool STD>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) void bulldozer_step_fused_kernel(
     gca_bulldozer_params p, const int32_t* __restrict__ action, double* __restrict__ accu, int32_t* __restrict__ steps,
     uint8_t* __restrict__ done, const double* __restrict__ wind, int64_t wind_stride, uint32_t* __restrict__ rng_step,
     uint8_t* __restrict__ parity, uint8_t* __restrict__ buf0, uint8_t* __restrict__ buf1, int H,
     int32_t* __restrict__ pos, int32_t* __restrict__ counts, uint8_t* __restrict__ hit, double* __restrict__ reward,
-    int64_t* __restrict__ steps_elapsed) {
+    int64_t* __restrict__ steps_elapsed, FusedPolicy pol) {
     constexpr int W = 256 * NW;
     __shared__ int32_t wave_cnt[16][3];  // per wave (no zeroing, no atomics): summed by thread 0 after the barrier
     const int e = blockIdx.x;
     const int tid = threadIdx.x;
     // ---- every per-env input (wave-uniform addresses: scalar loads), issued together
     const bool was_done = done[e] != 0;
-    const int32_t act0 = action[2 * e], act1 = action[2 * e + 1];
+    const uint32_t rs = rng_step[e];
+    int32_t act0, act1;
+    fused_action(action, pol, e, (uint32_t)(p.env_offset + e), rs, act0, act1);
+    if (pol.out && tid == 0) {
+        pol.out[2 * e] = act0;
+        pol.out[2 * e + 1] = act1;
+    }
     const double acc = accu[e];
     const bool odd = parity[e] != 0;
     const int32_t prow = pos[2 * e], pcol = pos[2 * e + 1];
     const int32_t c0 = counts[3 * e + 0], c1 = counts[3 * e + 1], c2 = counts[3 * e + 2];
-    const uint32_t rs = rng_step[e];
     const int64_t se = steps_elapsed ? steps_elapsed[e] : 0;
     double wl[9];
 #pragma unroll
@@ -598,7 +623,7 @@ __global__ __launch_bounds__(256) void bulldozer_step_fused_parts_kernel(
     uint8_t* __restrict__ done, const double* __restrict__ wind, int64_t wind_stride, uint32_t* __restrict__ rng_step,
     uint8_t* __restrict__ parity, uint8_t* __restrict__ buf0, uint8_t* __restrict__ buf1, int H,
     int32_t* __restrict__ pos, int32_t* __restrict__ counts, uint8_t* __restrict__ hit, double* __restrict__ reward,
-    int64_t* __restrict__ steps_elapsed, unsigned long long* __restrict__ meet) {
+    int64_t* __restrict__ steps_elapsed, unsigned long long* __restrict__ meet, FusedPolicy pol) {
     constexpr int W = 256 * NW;
     constexpr int SHv = (NW == 1 && P >= 4) ? 16 : FUSED_SH<NW>;
     constexpr int RDv = SHv < FUSED_RD<NW> ? SHv : FUSED_RD<NW>;
@@ -606,12 +631,17 @@ __global__ __launch_bounds__(256) void bulldozer_step_fused_parts_kernel(
     const int e = blockIdx.x / P, part = blockIdx.x - e * P;
     const int tid = threadIdx.x;
     const bool was_done = done[e] != 0;
-    const int32_t act0 = action[2 * e], act1 = action[2 * e + 1];
+    const uint32_t rs = rng_step[e];
+    int32_t act0, act1;
+    fused_action(action, pol, e, (uint32_t)(p.env_offset + e), rs, act0, act1);
+    if (pol.out && part == 0 && tid == 0) {
+        pol.out[2 * e] = act0;
+        pol.out[2 * e + 1] = act1;
+    }
     const double acc = accu[e];
     const bool odd = parity[e] != 0;
     const int32_t prow = pos[2 * e], pcol = pos[2 * e + 1];
     const int32_t c0 = counts[3 * e + 0], c1 = counts[3 * e + 1], c2 = counts[3 * e + 2];
-    const uint32_t rs = rng_step[e];
     const int64_t se = steps_elapsed ? steps_elapsed[e] : 0;
     double wl[9];
 #pragma unroll
@@ -795,12 +825,12 @@ extern "C" int gca_windy_step(uint8_t* buf0, uint8_t* buf1, const uint8_t* parit
     return GCA_OK;
 }
 
-extern "C" int gca_bulldozer_step_fused(const gca_bulldozer_params* p, const int32_t* action, double* accu,
-                                        int32_t* steps, uint8_t* done, const double* wind, int64_t wind_stride,
-                                        uint32_t* rng_step, uint8_t* parity, uint8_t* buf0, uint8_t* buf1, int H, int W,
-                                        int32_t* pos, int32_t* counts, uint8_t* hit, double* reward,
-                                        int64_t* steps_elapsed, uint64_t* meet, int E, void* stream) {
-    GCA_CHECK_ARG(p && action && accu && steps && done && wind && rng_step && parity && buf0 && buf1 && pos && counts &&
+static int bulldozer_step_fused_impl(const gca_bulldozer_params* p, const int32_t* action, FusedPolicy pol,
+                                     double* accu, int32_t* steps, uint8_t* done, const double* wind,
+                                     int64_t wind_stride, uint32_t* rng_step, uint8_t* parity, uint8_t* buf0,
+                                     uint8_t* buf1, int H, int W, int32_t* pos, int32_t* counts, uint8_t* hit,
+                                     double* reward, int64_t* steps_elapsed, uint64_t* meet, int E, void* stream) {
+    GCA_CHECK_ARG(p && accu && steps && done && wind && rng_step && parity && buf0 && buf1 && pos && counts &&
                       hit && reward && E > 0 && H > 0,
                   "bulldozer_step_fused: null argument or empty batch");
     GCA_CHECK_ARG(W == 256 || W == 512, "bulldozer_step_fused: W must be 256 or 512 (the row-stream CA)");
@@ -822,12 +852,12 @@ extern "C" int gca_bulldozer_step_fused(const gca_bulldozer_params* p, const int
 #define GCA_FUSED_LAUNCH(NWV, STDV)                                                                                 \
     hipLaunchKernelGGL((bulldozer_step_fused_kernel<NWV, STDV>), dim3((unsigned)E), dim3(threads), 0, st, *p, action, \
                        accu, steps, done, wind, wind_stride, rng_step, parity, buf0, buf1, H, pos, counts, hit, reward,   \
-                       steps_elapsed)
+                       steps_elapsed, pol)
     // with the caller's meeting slots: P workgroups per env (2 at W = 256, 4 at 512); without: one
 #define GCA_FUSED_PARTS_LAUNCH(NWV, STDV, PV)                                                                     \
     hipLaunchKernelGGL((bulldozer_step_fused_parts_kernel<NWV, STDV, PV>), dim3((unsigned)E * PV), dim3(256), 0, st, *p, \
                        action, accu, steps, done, wind, wind_stride, rng_step, parity, buf0, buf1, H, pos, counts, hit,  \
-                       reward, steps_elapsed, (unsigned long long*)meet)
+                       reward, steps_elapsed, (unsigned long long*)meet, pol)
     // the parts meet in 20-bit E / T / F fields of one 64-bit word per env: a field's total reaches H*W (+1 when Modify
     // moves an uncategorised code to a category), so grids of 2^20 - 1 cells or more take the one-workgroup kernel,
     // which sums in int32 (W = 256 at H >= 4096, W = 512 at H >= 2048); `meet` is then left untouched
@@ -849,4 +879,25 @@ extern "C" int gca_bulldozer_step_fused(const gca_bulldozer_params* p, const int
 #undef GCA_FUSED_PARTS_LAUNCH
     GCA_CHECK_LAUNCH("bulldozer_step_fused");
     return GCA_OK;
+}
+
+extern "C" int gca_bulldozer_step_fused(const gca_bulldozer_params* p, const int32_t* action, double* accu,
+                                        int32_t* steps, uint8_t* done, const double* wind, int64_t wind_stride,
+                                        uint32_t* rng_step, uint8_t* parity, uint8_t* buf0, uint8_t* buf1, int H, int W,
+                                        int32_t* pos, int32_t* counts, uint8_t* hit, double* reward,
+                                        int64_t* steps_elapsed, uint64_t* meet, int E, void* stream) {
+    GCA_CHECK_ARG(action, "bulldozer_step_fused: action required");
+    return bulldozer_step_fused_impl(p, action, FusedPolicy{0u, nullptr}, accu, steps, done, wind, wind_stride, rng_step,
+                                     parity, buf0, buf1, H, W, pos, counts, hit, reward, steps_elapsed, meet, E, stream);
+}
+
+extern "C" int gca_bulldozer_step_fused_random(const gca_bulldozer_params* p, uint64_t action_seed, int32_t* action_out,
+                                               double* accu, int32_t* steps, uint8_t* done, const double* wind,
+                                               int64_t wind_stride, uint32_t* rng_step, uint8_t* parity, uint8_t* buf0,
+                                               uint8_t* buf1, int H, int W, int32_t* pos, int32_t* counts, uint8_t* hit,
+                                               double* reward, int64_t* steps_elapsed, uint64_t* meet, int E,
+                                               void* stream) {
+    return bulldozer_step_fused_impl(p, nullptr, FusedPolicy{action_seed, action_out}, accu, steps, done, wind,
+                                     wind_stride, rng_step, parity, buf0, buf1, H, W, pos, counts, hit, reward,
+                                     steps_elapsed, meet, E, stream);
 }

@@ -91,6 +91,7 @@ class BatchedForestFireBulldozerEnv:
         self._ctx = {"wind": self.wind, "position": self.pos, "time": self.accu}
         self._fused_call = self._bound_meet = None
         self._sample_call = None
+        self._random_call = self._bound_meet_r = None
 
     # ------------------------------------------------------------------ state
     def grids(self):
@@ -168,6 +169,7 @@ class BatchedForestFireBulldozerEnv:
 
         self._fused_call = self._bound_meet = None
         self._sample_call = None
+        self._random_call = self._bound_meet_r = None
         self._done_bool = self.done.view(torch.bool)
         self._info = {"hit": self.hit, "ca_steps": self.steps}
         self._ctx = {"wind": self.wind, "position": self.pos, "time": self.accu}
@@ -182,6 +184,31 @@ class BatchedForestFireBulldozerEnv:
             dev.ptr(self.reward), dev.ptr(self.steps_elapsed), dev.ptr(meet) if meet is not None else None, E, SLOT)
         self._bound_meet = meet
         return self._fused_call
+
+    def step_random(self, seed=9, action_out=None):
+        """One env step of every env under a uniform random policy, the action drawn INSIDE the fused step
+        (gca_bulldozer_step_fused_random) exactly as sample_actions(out, tag=seed) draws it before step(out): the two
+        launches in one, bit for bit. The drawn actions go to `action_out` (a contiguous int32 (E, 2) device tensor,
+        default the env's action buffer). Fused step only (W = 256 / 512, one CA pass at most per env step)."""
+        if not self.fused:
+            raise ValueError("step_random needs the fused step (W in (256, 512), at most one CA pass per env step)")
+        out = self._act_buf if action_out is None else action_out
+        key = (seed, out.data_ptr(), self._meet is None)
+        if self._random_call is None or self._random_call[0] != key or self._bound_meet_r is not self._meet:
+            if not (dev.is_device_tensor(out) and out.is_contiguous() and out.numel() == 2 * self.num_envs
+                    and out.element_size() == 4 and not out.is_floating_point()):
+                raise ValueError("step_random: action_out must be a contiguous int32 (E, 2) device tensor")
+            E, H, W = self.num_envs, self.nrows, self.ncols
+            meet = self._meet
+            self._random_call = (key, BoundCall(
+                "gca_bulldozer_step_fused_random", self.params, int(seed) & (2**64 - 1), dev.ptr(out),
+                dev.ptr(self.accu), dev.ptr(self.steps), dev.ptr(self.done), dev.ptr(self.wind), 9,
+                dev.ptr(self.rng_step), dev.ptr(self.parity), dev.ptr(self.buf[0]), dev.ptr(self.buf[1]), H, W,
+                dev.ptr(self.pos), dev.ptr(self.counts), dev.ptr(self.hit), dev.ptr(self.reward),
+                dev.ptr(self.steps_elapsed), dev.ptr(meet) if meet is not None else None, E, SLOT))
+            self._bound_meet_r = meet
+        self._random_call[1](dev.raw_stream(self._dev_index))
+        return self._obs(), self.reward, self._done_bool, self._truncated, self._info
 
     def sample_actions(self, out=None, tag=9):
         """Uniform random actions for every env on the device -- the batched `action_space.sample()` (move in [0, 9),

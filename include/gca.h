@@ -131,6 +131,15 @@ int gca_bulldozer_step_fused(const gca_bulldozer_params* p, const int32_t* actio
                              uint8_t* parity, uint8_t* buf0, uint8_t* buf1, int H, int W, int32_t* pos,
                              int32_t* counts, uint8_t* hit, double* reward, int64_t* steps_elapsed, uint64_t* meet,
                              int E, void* stream);
+/* gca_bulldozer_step_fused under a random policy: every env's action is drawn inside the step exactly as
+ * gca_random_actions(action, E, p->env_offset, action_seed, rng_step) draws it before the step (move randint[0, 9),
+ * shoot the top bit, Philox keyed by the global env id and rng_step[e]) -- the pair of launches in one, bit for bit --
+ * and written to action_out (nullable, [E][2]). For random rollouts (action_space.sample() per env per step).       */
+int gca_bulldozer_step_fused_random(const gca_bulldozer_params* p, uint64_t action_seed, int32_t* action_out,
+                                    double* accu, int32_t* steps, uint8_t* done, const double* wind,
+                                    int64_t wind_stride, uint32_t* rng_step, uint8_t* parity, uint8_t* buf0,
+                                    uint8_t* buf1, int H, int W, int32_t* pos, int32_t* counts, uint8_t* hit,
+                                    double* reward, int64_t* steps_elapsed, uint64_t* meet, int E, void* stream);
 
 /* Move then Modify for E envs (move_modify.py:37-134): action[e] = (move, shoot);
  * uses p->up/down/left/right_mask and p->effect; grid may be NULL (Move only); hit nullable. */

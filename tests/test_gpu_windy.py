@@ -522,3 +522,35 @@ def test_rebind_after_replacing_a_state_tensor(device):
         for name in ("accu", "counts", "pos", "rng_step", "done"):
             assert torch.equal(getattr(envs[0], name), getattr(envs[1], name)), (name, s)
     assert envs[1]._ctx["time"] is envs[1].accu
+
+
+@pytest.mark.parametrize("N,parts", [(256, True), (512, True), (256, False)])
+def test_step_random_equals_sample_then_step(device, N, parts):
+    """gca_bulldozer_step_fused_random (env.step_random): the random policy's action drawn inside the fused step is
+    bit for bit env.sample_actions(a, seed) + env.step(a) -- every state tensor and the drawn actions after each of
+    40 env steps from a dense state, with and without the meeting slots."""
+    import torch
+
+    from gymca_amd.forest_fire.bulldozer import BatchedForestFireBulldozerEnv
+
+    E = 256
+    envs = [BatchedForestFireBulldozerEnv(E, N, N, device=device, seed=77, env_offset=5, materialize_obs=False)
+            for _ in range(2)]
+    for env in envs:
+        if not parts:
+            env._meet = None
+        env.reset(seed=6)
+        _dense_state(env, device, seed=31, p_fire=0.05)
+    a_ref = torch.zeros((E, 2), dtype=torch.int32, device=device)
+    a_got = torch.full((E, 2), -1, dtype=torch.int32, device=device)
+    ca = 0
+    for s in range(40):
+        envs[0].step(envs[0].sample_actions(a_ref, 17))
+        envs[1].step_random(17, a_got)
+        ca += int((envs[1].steps > 0).sum().item())
+        assert torch.equal(a_got, a_ref), s
+        assert torch.equal(envs[0].grids(), envs[1].grids()), s
+        for name in ("parity", "accu", "steps", "counts", "pos", "hit", "done", "rng_step", "steps_elapsed"):
+            assert torch.equal(getattr(envs[0], name), getattr(envs[1], name)), (name, s)
+        assert torch.equal(torch.nan_to_num(envs[0].reward), torch.nan_to_num(envs[1].reward)), s
+    assert ca > 40 * E // 40
