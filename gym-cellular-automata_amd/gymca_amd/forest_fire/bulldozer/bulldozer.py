@@ -105,6 +105,8 @@ class ForestFireBulldozerEnv(CAEnv):
         super().__init__(nrows, ncols, **kwargs)
         self.obs_device = bool(obs_device)
         self._counts = None  # this step's device count (Counter), shared by _is_done and _award
+        self._obs_host = None  # this step's observation, read back with the count
+        self._obs_pinned = None
         self.title = "ForestFireBulldozer" + str(nrows) + "x" + str(ncols)
         self._shoots = {"shoot": 1, "none": 0}
         self._empty, self._tree, self._fire = 0, 3, 25
@@ -148,13 +150,25 @@ class ForestFireBulldozerEnv(CAEnv):
         grid, ctx = obs
         if self.obs_device or not dev.is_device_tensor(grid):
             return obs
+        if self._obs_host is not None:  # read back with this step's count (_step_counts)
+            host, self._obs_host = self._obs_host, None
+            return host, ctx
         return grid.cpu().numpy().astype(TYPE_INT), ctx
 
     def step(self, action):
         self._to_device_grid()
         self.state = self.grid, self.context
         self._counts = None  # Modify edits the grid in place: the count is per step, not per grid object
-        obs, reward, terminated, truncated, info = super().step(action)
+        self._obs_host = None
+        # Move / Modify leave their read-back to this step's one synchronisation (_step_counts)
+        self.move_modify.defer_sync = True
+        try:
+            obs, reward, terminated, truncated, info = super().step(action)
+        finally:
+            self.move_modify.defer_sync = False
+            io = self.move_modify._io
+            if io is not None and io.pending is not None:  # a step that never counted (done on entry, an error)
+                io.sync_read()
         return self._host_obs(obs), reward, terminated, truncated, info
 
     def reset(self, *, seed=None, options=None):
@@ -174,10 +188,35 @@ class ForestFireBulldozerEnv(CAEnv):
         self.done = not bool(self._step_counts()[self._fire])
 
     def _step_counts(self):
-        """One gca_count_cells per step: _is_done and then _award read the same count of the same grid."""
+        """One gca_count_cells per step: _is_done and then _award read the same count of the same grid. On the
+        device the count, Move / Modify's position and hit and (unless obs_device) the observation come back in
+        ONE synchronisation, through the MoveModify operator's pinned DeviceIO."""
         if self._counts is None:
-            self._counts = self.count_cells(self.grid)
+            io = self.move_modify._io
+            g = self.grid
+            if io is not None and dev.is_device_tensor(g) and g.device == io.device and g.is_contiguous():
+                self._counts = self._count_with(io, g)
+            else:
+                self._counts = self.count_cells(self.grid)
         return self._counts
+
+    def _count_with(self, io, g):
+        import torch
+        from collections import Counter
+
+        H, W = g.shape[-2:]
+        call("gca_count_cells", dev.ptr(g), 1, H, W, self._empty, self._tree, self._fire, io.p_counts,
+             dev.stream_ptr(io.device))
+        extra = ()
+        if not self.obs_device:
+            if self._obs_pinned is None or tuple(self._obs_pinned.shape) != tuple(g.shape):
+                self._obs_pinned = torch.empty(tuple(g.shape), dtype=torch.uint8, pin_memory=True)
+            extra = ((self._obs_pinned, g),)
+        out = io.sync_read(extra)
+        if extra:
+            self._obs_host = self._obs_pinned.numpy().astype(TYPE_INT)
+        c = out[5:8].tolist()
+        return Counter({v: n for v, n in zip((self._empty, self._tree, self._fire), c) if n})
 
     def _report(self):
         return {"hit": self.modify.hit}

@@ -53,6 +53,7 @@ class WindyForestFire(Operator):
             self.context_space = Box(0.0, 1.0, shape=(3, 3), dtype=TYPE_BOX)
         self._calls = 0
         self.roll_queue = []  # rolls injected in FIFO order (golden-vector replay of env episodes)
+        self._wind_d = None  # (key, device wind) of the last call
 
     # ------------------------------------------------------------------ API
     def update(self, grid, action, wind, *, roll=None):
@@ -78,7 +79,11 @@ class WindyForestFire(Operator):
                 raise ValueError("cell values must fit the u8 device layout (0..255)")
             src = dev.to_device(g.reshape(E, H, W).astype(np.uint8), torch.uint8, device)
         dst = torch.empty_like(src)
-        wind_d = dev.to_device(np.broadcast_to(np.asarray(w, dtype=np.float64), (E, 3, 3)), torch.float64, device)
+        w64 = np.asarray(w, dtype=np.float64)
+        key = (E, str(device), w64.shape, w64.tobytes())
+        if self._wind_d is None or self._wind_d[0] != key:  # the env's wind rarely changes: upload it once
+            self._wind_d = (key, dev.to_device(np.broadcast_to(w64, (E, 3, 3)), torch.float64, device))
+        wind_d = self._wind_d[1]
         roll_d = None
         if roll is None and self.roll_queue:
             roll = self.roll_queue.pop(0)

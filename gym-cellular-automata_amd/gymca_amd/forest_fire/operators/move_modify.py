@@ -92,8 +92,57 @@ def _run_host(params, grid, action_pair, position, with_grid):
     return pos[0].astype(np.int64), bool(hit[0])
 
 
-def _run(params, grid, action_pair, position, with_grid, backend=None):
-    """One env through gca_move_modify. Returns (new_position, hit); the grid is modified in place."""
+class DeviceIO:
+    """One env's Move / Modify operands and results, staged through pinned host memory: int32[8] =
+    [move, shoot, row, col, hit (u8 in the low byte), n_empty, n_tree, n_fire] on the device, one pinned copy each
+    way. A call costs one H2D copy, the launch, one D2H copy and ONE synchronisation (the eager version cost two
+    pageable uploads and two synchronising reads). `pending` defers even that synchronisation: the bulldozer env
+    reads the position and hit back together with its cell count and observation (bulldozer.py, _step_counts)."""
+
+    def __init__(self, device):
+        import torch
+
+        self.device = device
+        self.h_in = torch.zeros(8, dtype=torch.int32, pin_memory=True)
+        self.h_out = torch.zeros(8, dtype=torch.int32, pin_memory=True)
+        self.d = torch.zeros(8, dtype=torch.int32, device=device)
+        self.n_in, self.n_out = self.h_in.numpy(), self.h_out.numpy()
+        base = self.d.data_ptr()
+        self.p_act, self.p_pos, self.p_hit, self.p_counts = base, base + 8, base + 16, base + 20
+        self.in_flight = False  # h_in has been handed to a copy that no synchronisation has covered yet
+        self.pending = None  # (position array to fill, Modify whose hit to set) of a deferred call
+
+    def stage(self, a0, a1, row, col):
+        if self.in_flight:  # the previous call's upload must have run before its pinned source is rewritten
+            self.sync_read()
+        self.n_in[:] = (a0, a1, row, col, 0, 0, 0, 0)
+        self.d.copy_(self.h_in, non_blocking=True)
+        self.in_flight = True
+
+    def sync_read(self, extra=()):
+        """D2H of the results (+ `extra` (pinned dst, device src) pairs), one synchronisation, deferred results
+        filled in. Returns the host int32[8]."""
+        import torch
+
+        self.h_out.copy_(self.d, non_blocking=True)
+        for dst, src in extra:
+            dst.copy_(src, non_blocking=True)
+        torch.cuda.current_stream(self.device).synchronize()
+        self.in_flight = False
+        if self.pending is not None:
+            pos, modify = self.pending
+            self.pending = None
+            pos[0], pos[1] = int(self.n_out[2]), int(self.n_out[3])
+            if modify is not None:
+                modify.hit = bool(self.n_out[4])
+        return self.n_out
+
+
+def _run(params, grid, action_pair, position, with_grid, backend=None, io=None, defer=None):
+    """One env through gca_move_modify. Returns (new_position, hit); the grid is modified in place.
+    `io` (DeviceIO) stages a device grid's call through pinned memory; with `defer` = the Modify to update, the
+    synchronisation is left to the caller's next io.sync_read(): the returned position array is filled, and
+    defer.hit set, then (hit is returned as None)."""
     import torch
 
     on_device = dev.is_device_tensor(grid)
@@ -102,6 +151,22 @@ def _run(params, grid, action_pair, position, with_grid, backend=None):
     device = dev.require_device()
     shape = tuple(grid.shape)
     H, W = shape[-2:]
+    if on_device and io is not None:
+        r, c = int(position[0]), int(position[1])
+        if with_grid:
+            if grid.dtype != torch.uint8 or not grid.is_contiguous():
+                raise ValueError("device grids must be contiguous uint8 tensors")
+            if not (0 <= r < H and 0 <= c < W):  # moves stay in bounds (move_modify.py:37-67); the start must be
+                raise GCAError(f"move_modify: position ({r}, {c}) outside the {H}x{W} grid")
+        io.stage(int(action_pair[0]), int(bool(action_pair[1])), r, c)
+        call("gca_move_modify", params, io.p_act, io.p_pos, dev.ptr(grid) if with_grid else None, H, W, io.p_hit, 1,
+             dev.stream_ptr(device))
+        if defer is not None:
+            new_pos = np.empty(2, dtype=np.int64)
+            io.pending = (new_pos, defer)
+            return new_pos, None
+        out = io.sync_read()
+        return out[2:4].astype(np.int64), bool(out[4])
     act = torch.tensor([[int(action_pair[0]), int(bool(action_pair[1]))]], dtype=torch.int32, device=device)
     pos = torch.tensor([[int(position[0]), int(position[1])]], dtype=torch.int32, device=device)
     hit = torch.zeros(1, dtype=torch.uint8, device=device)
@@ -184,6 +249,10 @@ class MoveModify(Operator):
         self.move = move
         self.modify = modify
         self._fused = None
+        self._io = None  # DeviceIO of the fused device call, made on first use
+        # set by an env that reads the results back itself (ForestFireBulldozerEnv.step): the returned position is
+        # filled, and modify.hit set, by that env's next self._io.sync_read()
+        self.defer_sync = False
         if self.action_space is None:
             if self.move.action_space is not None and self.move.action_space is not None:
                 self.action_space = Tuple((self.move.action_space, self.move.action_space))
@@ -203,9 +272,16 @@ class MoveModify(Operator):
                 self._fused = make_params(d, self.modify.effects)
             shoot = bool(modify_action)
             backend = self.move.backend if self.move.backend == self.modify.backend else None
+            io = None
+            if dev.is_device_tensor(grid):
+                if self._io is None or self._io.device != grid.device:
+                    self._io = DeviceIO(grid.device)
+                io = self._io
+            defer = self.modify if (self.defer_sync and io is not None) else None
             position, hit = _run(self._fused, grid, (int(move_action), int(shoot)), position, with_grid=shoot,
-                                 backend=backend)
-            self.modify.hit = hit
+                                 backend=backend, io=io, defer=defer)
+            if defer is None:
+                self.modify.hit = hit
             return grid, position
         grid, position = self.move(grid, move_action, position)
         grid, position = self.modify(grid, modify_action, position)

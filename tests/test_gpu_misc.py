@@ -37,6 +37,59 @@ def test_move_modify_dropins_match_reference_rows(golden, device):
         assert tuple(pos) == (pr, pc) and g is grid and grid[pr, pc] == after and mm.modify.hit == bool(hit)
 
 
+def test_move_modify_device_grid_through_pinned_staging(golden, device):
+    """The device-grid call (DeviceIO: one pinned upload, one read-back) on the same golden rows, and a start
+    position outside the grid refused on the host before any launch."""
+    import torch
+
+    from gymca_amd._lib import GCAError
+    from gymca_amd.forest_fire.operators import Modify, Move, MoveModify
+
+    sets = {"up": {0, 1, 2}, "down": {6, 7, 8}, "left": {0, 3, 6}, "right": {2, 5, 8}, "not_move": {4}}
+    mm = MoveModify(Move(sets), Modify({3: 0}))
+    rows = golden("move_modify")["rows"]
+    rng = np.random.default_rng(1)
+    for H, W, r, c, a, shoot, pr, pc, before, after, hit in rows[rng.choice(len(rows), 200, replace=False)]:
+        grid = torch.zeros((H, W), dtype=torch.uint8, device=device)
+        grid[pr, pc] = int(before)
+        g, pos = mm(grid, (int(a), int(shoot)), np.array([r, c]))
+        assert g is grid and tuple(pos) == (pr, pc) and pos.dtype == np.int64
+        assert int(grid[pr, pc]) == after and mm.modify.hit == bool(hit)
+    grid = torch.zeros((4, 4), dtype=torch.uint8, device=device)
+    with pytest.raises(GCAError):
+        mm(grid, (4, 1), np.array([4, 0]))
+
+
+def test_dropin_bulldozer_one_readback_per_step(device):
+    """ForestFireBulldozerEnv on the device reads the count, Move / Modify's position and hit and the observation
+    back in one synchronisation: the values equal what the env state holds afterwards, each step returns its own
+    position array, and obs_device=True returns the device grid."""
+    import torch
+
+    from gymca_amd.forest_fire.bulldozer import ForestFireBulldozerEnv
+
+    for obs_device in (False, True):
+        env = ForestFireBulldozerEnv(32, 32, obs_device=obs_device)
+        env.reset(seed=3)
+        seen = []
+        for s in range(40):
+            obs, rew, term, trunc, info = env.step(np.array([s % 9, s % 2]))
+            grid, (_, pos, _) = obs
+            assert torch.is_tensor(grid) == obs_device
+            host = grid.cpu().numpy() if obs_device else grid
+            assert np.array_equal(host, env.grid.cpu().numpy())
+            assert pos.shape == (2,) and np.all((0 <= pos) & (pos < 32)) and all(p is not pos for p in seen)
+            assert np.array_equal(pos, env.context[1]) and isinstance(info["hit"], bool)
+            counts = env.count_cells(env.grid)
+            assert term == (counts[25] == 0)
+            if not term:
+                assert rew == -(counts[25] / (counts[3] + counts[25]))
+            seen.append(pos)
+            if term:
+                break
+        assert env.move_modify._io.pending is None and not env.move_modify._io.in_flight
+
+
 def test_modify_cyclic_effects_reference_test(device):
     """test_move_modify.py:92-125: cyclic effects on a 3-state grid, in place."""
     from gymca_amd.forest_fire.operators import Modify
