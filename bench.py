@@ -896,7 +896,8 @@ def bench_dropins(device):
     dt = time.perf_counter() - t0
     out["bulldozer_256"] = {"env_steps_per_s": steps / dt, "steps": steps, "resets": resets,
                             "note": "ForestFireBulldozerEnv(256, 256) drop-in, numpy int64 obs per step, grid "
-                                    "device-resident, one cell count per step"}
+                                    "device-resident; the cell count, position, hit and observation read back in one "
+                                    "synchronisation per step"}
     heli = ForestFireHelicopterEnv(5, 5)
     heli.reset(seed=0)
     heli.step(0)
