@@ -6,6 +6,8 @@
 //          arrays — 7 load streams per wave at 256 KiB-or-more strides;
 //   L = 1  the read-only fields of a row interleaved in one block: [plane 0..3 of row r (4 KiB) | vd of row r
 //          (256 B) | dousing bits of row r (32 B)], rows consecutive — one read-only stream per wave.
+// FRAME: the fused frame's extra stream, each row's f32 RGB (12 B/cell) as three contiguous 1-KiB dwordx4 stores per
+// wave (the pattern the frame's LDS transposition produces), at 2 / 3 / 4 waves per SIMD.
 // HIP events, mean of 10 launches after 3. Build: hipcc -O3 --offload-arch=gfx950 scripts/layout_probe.hip -o
 // scripts/layout_probe. Prints one JSON line (ms per launch).
 #include <hip/hip_runtime.h>
@@ -21,11 +23,11 @@ constexpr int E = 4096, H = 256, W = 256, R = 6;
 constexpr size_t HW = (size_t)H * W, N = (size_t)E * HW;
 constexpr size_t ROWB = 4 * 4 * W + W + W / 8;  // L = 1: bytes of one row's read-only block (4384)
 
-template <int SH, int L>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void probe_k(
+template <int SH, int L, int OCC, bool FRAME>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void probe_k(
     const uint8_t* __restrict__ g, uint8_t* __restrict__ go, const int16_t* __restrict__ a, int16_t* __restrict__ ao,
     const uint8_t* __restrict__ vd, const uint16_t* __restrict__ db, const vf4* __restrict__ es,
-    const uint8_t* __restrict__ st) {
+    const uint8_t* __restrict__ st, vf4* __restrict__ rgb) {
     constexpr int SPE = H / SH;
     const int wv = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int e = wv / SPE, s0 = (wv - e * SPE) * SH;
@@ -94,6 +96,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
         vu2 aa = ag[i & 1];
         aa.x ^= mix;
         __builtin_nontemporal_store(aa, reinterpret_cast<vu2*>(ao + e * HW + lo));
+        if constexpr (FRAME) {  // the row's f32 RGB, 3 KiB contiguous: three 1-KiB dwordx4 stores per wave
+            vf4* fr = rgb + ((size_t)e * HW + (size_t)r * W) * 3 / 4;
+            const float m = (float)(own ^ mix);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) __builtin_nontemporal_store((vf4){m, acc, m, (float)k}, fr + 64 * k + lane);
+        }
         __builtin_amdgcn_sched_barrier(0);
     }
 }
@@ -115,6 +123,7 @@ static float time_ms(F launch) {
 
 int main() {
     uint8_t *g, *go, *vd, *st;
+    vf4* rgb;
     int16_t *a, *ao;
     uint16_t* db;
     vf4* es;
@@ -126,6 +135,7 @@ int main() {
     CK(hipMalloc(&db, N / 8));
     CK(hipMalloc(&es, 16 * N));
     CK(hipMalloc(&st, (size_t)E * H * ROWB));
+    CK(hipMalloc(&rgb, 12 * N));
     CK(hipMemset(g, 1, N));
     CK(hipMemset(vd, 2, N));
     CK(hipMemset(a, 0, 2 * N));
@@ -133,10 +143,12 @@ int main() {
     CK(hipMemset(es, 0, 16 * N));
     CK(hipMemset(st, 0, (size_t)E * H * ROWB));
     printf("{\"cells\": %zu, \"bytes_per_cell\": 23.125", N);
-#define P(SH, L) printf(", \"sh%d_L%d_ms\": %.4f", SH, L, time_ms([&] { \
-        hipLaunchKernelGGL((probe_k<SH, L>), dim3(E * (H / SH) / 4), dim3(256), 0, 0, g, go, a, ao, vd, db, es, st); }))
+#define P(SH, L, OCC, FR) printf(", \"sh%d_L%d_occ%d%s_ms\": %.4f", SH, L, OCC, FR ? "_frame" : "", time_ms([&] { \
+        hipLaunchKernelGGL((probe_k<SH, L, OCC, FR>), dim3(E * (H / SH) / 4), dim3(256), 0, 0, g, go, a, ao, vd, db, es, \
+                           st, rgb); }))
     for (int rep = 0; rep < 2; ++rep) {
-        P(16, 0); P(16, 1); P(32, 0); P(32, 1);
+        P(16, 0, 3, false); P(16, 1, 3, false); P(32, 0, 3, false); P(32, 1, 3, false);
+        P(16, 0, 2, true); P(16, 0, 3, true); P(16, 0, 4, true);
     }
     printf("}\n");
     return 0;
