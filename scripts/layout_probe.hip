@@ -7,7 +7,8 @@
 //   L = 1  the read-only fields of a row interleaved in one block: [plane 0..3 of row r (4 KiB) | vd of row r
 //          (256 B) | dousing bits of row r (32 B)], rows consecutive — one read-only stream per wave.
 // FRAME: the fused frame's extra stream, each row's f32 RGB (12 B/cell) as three contiguous 1-KiB dwordx4 stores per
-// wave (the pattern the frame's LDS transposition produces), at 2 / 3 / 4 waves per SIMD.
+// wave (the pattern the frame's LDS transposition produces), at 2 / 3 / 4 waves per SIMD; POL = the frame stores'
+// cache policy: 0 nt (the kernel's), 1 default, 2 sc1, 3 sc0 sc1, 4 sc1 nt.
 // HIP events, mean of 10 launches after 3. Build: hipcc -O3 --offload-arch=gfx950 scripts/layout_probe.hip -o
 // scripts/layout_probe. Prints one JSON line (ms per launch).
 #include <hip/hip_runtime.h>
@@ -23,7 +24,7 @@ constexpr int E = 4096, H = 256, W = 256, R = 6;
 constexpr size_t HW = (size_t)H * W, N = (size_t)E * HW;
 constexpr size_t ROWB = 4 * 4 * W + W + W / 8;  // L = 1: bytes of one row's read-only block (4384)
 
-template <int SH, int L, int OCC, bool FRAME>
+template <int SH, int L, int OCC, bool FRAME, int POL = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void probe_k(
     const uint8_t* __restrict__ g, uint8_t* __restrict__ go, const int16_t* __restrict__ a, int16_t* __restrict__ ao,
     const uint8_t* __restrict__ vd, const uint16_t* __restrict__ db, const vf4* __restrict__ es,
@@ -100,7 +101,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
             vf4* fr = rgb + ((size_t)e * HW + (size_t)r * W) * 3 / 4;
             const float m = (float)(own ^ mix);
 #pragma unroll
-            for (int k = 0; k < 3; ++k) __builtin_nontemporal_store((vf4){m, acc, m, (float)k}, fr + 64 * k + lane);
+            for (int k = 0; k < 3; ++k) {
+                const vf4 v = (vf4){m, acc, m, (float)k};
+                vf4* dst = fr + 64 * k + lane;
+                if constexpr (POL == 0) __builtin_nontemporal_store(v, dst);
+                else if constexpr (POL == 1) *dst = v;
+                else if constexpr (POL == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1" :: "v"(dst), "v"(v) : "memory");
+                else if constexpr (POL == 3) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" :: "v"(dst), "v"(v) : "memory");
+                else asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" :: "v"(dst), "v"(v) : "memory");
+            }
         }
         __builtin_amdgcn_sched_barrier(0);
     }
@@ -143,12 +152,12 @@ int main() {
     CK(hipMemset(es, 0, 16 * N));
     CK(hipMemset(st, 0, (size_t)E * H * ROWB));
     printf("{\"cells\": %zu, \"bytes_per_cell\": 23.125", N);
-#define P(SH, L, OCC, FR) printf(", \"sh%d_L%d_occ%d%s_ms\": %.4f", SH, L, OCC, FR ? "_frame" : "", time_ms([&] { \
-        hipLaunchKernelGGL((probe_k<SH, L, OCC, FR>), dim3(E * (H / SH) / 4), dim3(256), 0, 0, g, go, a, ao, vd, db, es, \
-                           st, rgb); }))
+#define P(SH, L, OCC, FR, POL) printf(", \"sh%d_L%d_occ%d%s_pol%d_ms\": %.4f", SH, L, OCC, FR ? "_frame" : "", POL, \
+        time_ms([&] { hipLaunchKernelGGL((probe_k<SH, L, OCC, FR, POL>), dim3(E * (H / SH) / 4), dim3(256), 0, 0, g, go, \
+                                         a, ao, vd, db, es, st, rgb); }))
     for (int rep = 0; rep < 2; ++rep) {
-        P(16, 0, 3, false); P(16, 1, 3, false); P(32, 0, 3, false); P(32, 1, 3, false);
-        P(16, 0, 2, true); P(16, 0, 3, true); P(16, 0, 4, true);
+        P(16, 0, 3, false, 0);
+        P(16, 0, 2, true, 0); P(16, 0, 2, true, 1); P(16, 0, 2, true, 2); P(16, 0, 2, true, 3); P(16, 0, 2, true, 4);
     }
     printf("}\n");
     return 0;
