@@ -44,7 +44,7 @@ import numpy as np
 from ... import _device as dev
 from ..._lib import AdvEnvParams, call
 from ..._seeding import env_integers
-from ..operators.ca_alexandridis import alex_constants, make_alex_params
+from ..operators.ca_alexandridis import make_alex_params
 from .bulldozer import ACTION_SETS, bulldozer_timings
 from .init_utils import altitude_plan, device_altitude, get_winds, init_density, init_vegetation
 from .observation import make_obs_params

@@ -2,7 +2,6 @@
 import numpy as np
 
 from oracle import alexandridis_ref as ref
-from oracle.philox import philox4x32_10
 
 
 def winds():
