@@ -81,7 +81,7 @@ __global__ void bulldozer_post_kernel(gca_bulldozer_params p, int last_pass, con
     pos[2 * e] = row;
     pos[2 * e + 1] = col;
     uint8_t h = 0;
-    if (a1) {
+    if (a1 && row >= 0 && row < H && col >= 0 && col < W) {  // a caller's own out-of-grid position writes nothing
         const int v = grid[(int64_t)row * W + col];
         const int nv = p.effect[v];
         if (nv >= 0) {
@@ -164,7 +164,7 @@ __global__ void advenv_post_kernel(gca_advenv_params p, const int32_t* __restric
     move_pos(a0, row, col, H, W, p.up_mask, p.down_mask, p.left_mask, p.right_mask);
     pos[2 * e] = row;
     pos[2 * e + 1] = col;
-    if (a1 == 1) {
+    if (a1 == 1 && row >= 0 && row < H && col >= 0 && col < W) {  // JAX drops out-of-bounds scatter updates
         const int64_t cell = (int64_t)e * H * W + (int64_t)row * W + col;
         dousing[cell] = 1;
         if (dous_bits) dous_bits[cell >> 4] |= (uint16_t)(1u << (cell & 15));  // packed layout (one writer per env)
@@ -271,7 +271,9 @@ __global__ void move_modify_kernel(const int32_t* __restrict__ action, int32_t* 
     pos[2 * e] = row;
     pos[2 * e + 1] = col;
     uint8_t h = 0;
-    if (grid && a1) {
+    // a caller's own start outside the grid that no move brings inside: no write (the host build and the Python
+    // layer refuse it with GCA_ERR_ARG before any launch; a kernel cannot, so it only stays inside the buffer)
+    if (grid && a1 && row >= 0 && row < H && col >= 0 && col < W) {
         uint8_t* g = grid + (int64_t)e * H * W + (int64_t)row * W + col;
         const int nv = p.effect[*g];
         if (nv >= 0) {

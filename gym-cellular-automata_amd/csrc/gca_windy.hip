@@ -587,7 +587,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
     pos[2 * e] = row;
     pos[2 * e + 1] = col;
     uint8_t h = 0;
-    if (act1) {
+    // a position outside the grid (a caller's own, never produced by Move from inside) writes nothing
+    if (act1 && row >= 0 && row < H && col >= 0 && col < W) {
         const int v = grid[(int64_t)row * W + col];
         const int nv = p.effect[v];
         if (nv >= 0) {
@@ -696,7 +697,7 @@ __global__ __launch_bounds__(256) void bulldozer_step_fused_parts_kernel(
         pE = pT = pF = 1;
     }
     const int owner = min((row / SHv) / spp, P - 1);
-    if (n >= 0 && part == owner && act1) {
+    if (n >= 0 && part == owner && act1 && row >= 0 && row < H && col >= 0 && col < W) {  // (no write outside the grid)
         const int v = grid[(int64_t)row * W + col];
         const int nv = p.effect[v];
         if (nv >= 0) {

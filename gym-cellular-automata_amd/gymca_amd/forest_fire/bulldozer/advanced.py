@@ -303,6 +303,9 @@ class AdvancedForestFireBulldozerEnv:
         self.age[0].index_put_(idx, torch.tensor((H + H // 2) * 2, dtype=torch.int16, device=self.device))
         # bulldozer: pos_bull[env], default (int(0.15 N), int(0.85 N)) (:690-700)
         bull = self._pos_bull if self._pos_bull is not None else [(int(H * 0.15), int(W * 0.85))] * E
+        b = np.asarray(bull, np.int64).reshape(E, 2)
+        if ((b[:, 0] < 0) | (b[:, 0] >= H) | (b[:, 1] < 0) | (b[:, 1] >= W)).any():
+            raise ValueError(f"pos_bull holds a position outside the {H}x{W} grid")
         self.pos.copy_(torch.as_tensor(np.asarray(bull, np.int32).reshape(E, 2), device=self.device))
         # initial wind index per env (:703-709), keyed by the global env id (shard-invariant)
         wi = (env_integers(self.key if seed is None else int(seed), self.env_offset, E, 0x57494E44, 0, 8)
@@ -358,6 +361,9 @@ class AdvancedForestFireBulldozerEnv:
                 raise ValueError("the packed layout stores dousing counts as bits: values must be 0/1 "
                                  "(use slope_layout='edge' for other counts)")
         if position is not None:
+            pt = (position if dev.is_device_tensor(position) else torch.as_tensor(np.asarray(position))).reshape(-1, 2)
+            if bool(((pt[:, 0] < 0) | (pt[:, 0] >= self.nrows) | (pt[:, 1] < 0) | (pt[:, 1] >= self.ncols)).any()):
+                raise ValueError(f"position: every (row, col) must lie inside the {self.nrows}x{self.ncols} grid")
             put(self.pos, position, torch.int32)
         if altitude is not None:
             alt = altitude if dev.is_device_tensor(altitude) else torch.as_tensor(np.asarray(altitude, np.float64),
@@ -489,7 +495,10 @@ class AdvancedForestFireBulldozerEnv:
             src_of(pe.get("is_night"), "is_night", self.is_night, (0, 1))
             src_of(pe.get("time_step"), "time_step", self.time_step)
             src_of(pe.get("key"), "key", self.rng_step)
-            src_of(ctx.get("position"), "position", self.pos)
+            src_of(ctx.get("position"), "position", self.pos, (0, max(H, W) - 1))
+            for name, t, _ in plan:  # rows and columns each inside the grid (the kernels' scatters assume it)
+                if name == "position" and t.numel() and (bool((t[:, 0] >= H).any()) or bool((t[:, 1] >= W).any())):
+                    raise ValueError(f"position: every (row, col) must lie inside the {H}x{W} grid")
             src_of(ctx.get("time"), "time", self.accu)
             if obs[0] is not None and self.rgb is not None:
                 src_of(obs[0], "rgb", self.rgb)

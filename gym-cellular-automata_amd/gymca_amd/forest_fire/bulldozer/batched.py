@@ -129,6 +129,8 @@ class BatchedForestFireBulldozerEnv:
                 self._fire
         if positions is not None:
             pos = np.asarray(positions).reshape(E, 2)
+            if not ((pos[:, 0] >= 0) & (pos[:, 0] < H) & (pos[:, 1] >= 0) & (pos[:, 1] < W)).all():
+                raise ValueError(f"reset: every position must lie inside the {H}x{W} grid")
         else:
             pos = np.stack([H // 4 + noise(3, H), 3 * W // 4 + noise(4, W)], axis=1)
         self.pos.copy_(torch.as_tensor(pos.astype(np.int32), device=self.device))

@@ -138,6 +138,17 @@ class DeviceIO:
         return self.n_out
 
 
+def _moved(params, a, row, col, H, W):
+    """Move's arithmetic (move_modify.py:37-67) on the host, for validating a position before a device Modify."""
+    if 0 <= a < 32:
+        vu, vd, vl, vr = row > 0, row < H - 1, col > 0, col < W - 1
+        row -= 1 if (params.up_mask >> a) & 1 and vu else 0
+        row += 1 if (params.down_mask >> a) & 1 and vd else 0
+        col -= 1 if (params.left_mask >> a) & 1 and vl else 0
+        col += 1 if (params.right_mask >> a) & 1 and vr else 0
+    return row, col
+
+
 def _run(params, grid, action_pair, position, with_grid, backend=None, io=None, defer=None):
     """One env through gca_move_modify. Returns (new_position, hit); the grid is modified in place.
     `io` (DeviceIO) stages a device grid's call through pinned memory; with `defer` = the Modify to update, the
@@ -156,8 +167,10 @@ def _run(params, grid, action_pair, position, with_grid, backend=None, io=None, 
         if with_grid:
             if grid.dtype != torch.uint8 or not grid.is_contiguous():
                 raise ValueError("device grids must be contiguous uint8 tensors")
-            if not (0 <= r < H and 0 <= c < W):  # moves stay in bounds (move_modify.py:37-67); the start must be
-                raise GCAError(f"move_modify: position ({r}, {c}) outside the {H}x{W} grid")
+            if not (0 <= r < H and 0 <= c < W):  # a caller's own out-of-grid start: refused, like the host build,
+                mr, mc = _moved(params, int(action_pair[0]), r, c, H, W)  # unless the move brings it inside
+                if not (0 <= mr < H and 0 <= mc < W):
+                    raise GCAError(f"move_modify: position ({mr}, {mc}) outside the {H}x{W} grid")
         io.stage(int(action_pair[0]), int(bool(action_pair[1])), r, c)
         call("gca_move_modify", params, io.p_act, io.p_pos, dev.ptr(grid) if with_grid else None, H, W, io.p_hit, 1,
              dev.stream_ptr(device))

@@ -57,7 +57,46 @@ def test_move_modify_device_grid_through_pinned_staging(golden, device):
         assert int(grid[pr, pc]) == after and mm.modify.hit == bool(hit)
     grid = torch.zeros((4, 4), dtype=torch.uint8, device=device)
     with pytest.raises(GCAError):
-        mm(grid, (4, 1), np.array([4, 0]))
+        mm(grid, (4, 1), np.array([4, 0]))  # not_move from row 4 of a 4-row grid
+    grid[3, 0] = 3
+    g, pos = mm(grid, (1, 1), np.array([4, 0]))  # up from row 4 lands on row 3, as in the host build
+    assert tuple(pos) == (3, 0) and int(grid[3, 0]) == 0 and mm.modify.hit
+
+
+def test_positions_outside_the_grid_write_nothing(device):
+    """Out-of-grid positions: the C-ABI kernels write nothing (the raw call, no host check in between), and the
+    env entry points that take a caller's positions refuse them before any launch."""
+    import torch
+
+    from gymca_amd import _device as dev
+    from gymca_amd._lib import call
+    from gymca_amd.forest_fire.bulldozer import AdvancedForestFireBulldozerEnv, BatchedForestFireBulldozerEnv
+    from gymca_amd.forest_fire.operators.move_modify import make_params
+
+    E, H, W = 4, 8, 8
+    p = make_params({"up": {0, 1, 2}, "down": {6, 7, 8}, "left": {0, 3, 6}, "right": {2, 5, 8}}, {3: 0})
+    grid = torch.full((E, H, W), 3, dtype=torch.uint8, device=device)  # an unguarded write would land in env e +- 1
+    act = torch.tensor([[4, 1]] * E, dtype=torch.int32, device=device)  # not_move, shoot
+    pos = torch.tensor([[H, 0], [-1, 3], [2, W], [3, -1]], dtype=torch.int32, device=device)
+    hit = torch.ones(E, dtype=torch.uint8, device=device)
+    call("gca_move_modify", p, dev.ptr(act), dev.ptr(pos), dev.ptr(grid), H, W, dev.ptr(hit), E, dev.stream_ptr())
+    torch.cuda.synchronize()
+    assert bool((grid == 3).all()) and int(hit.sum()) == 0
+    env = BatchedForestFireBulldozerEnv(2, 256, 256, device=device, materialize_obs=False)
+    with pytest.raises(ValueError):
+        env.reset(positions=[[0, 0], [256, 3]])
+    adv = AdvancedForestFireBulldozerEnv(16, 16, key=1, num_envs=2, use_hidden=False, device=device, observation="grid")
+    obs, info = adv.reset()
+    with pytest.raises(ValueError):
+        adv.set_state(position=[[0, 0], [3, 16]])
+    adv.stateless_step(torch.zeros((2, 3), dtype=torch.int32, device=device), obs, info)  # the valid call runs
+    bad = dict(obs[1])
+    bad["position"] = torch.tensor([[0, 0], [16, 1]], dtype=torch.int32, device=device)
+    with pytest.raises(ValueError):
+        adv.stateless_step(torch.zeros((2, 3), dtype=torch.int32, device=device), (obs[0], bad), info)
+    with pytest.raises(ValueError):
+        AdvancedForestFireBulldozerEnv(16, 16, key=1, num_envs=2, use_hidden=False, device=device,
+                                       pos_bull=[(0, 0), (0, 16)]).reset()
 
 
 def test_dropin_bulldozer_one_readback_per_step(device):
