@@ -354,6 +354,9 @@ class AdvancedForestFireBulldozerEnv:
         if density is not None:
             put(self.density, density, torch.uint8)
         if wind_index is not None:
+            wt = wind_index if dev.is_device_tensor(wind_index) else torch.as_tensor(np.asarray(wind_index))
+            if wt.numel() and (bool((wt < 0).any()) or bool((wt >= len(self._winds)).any())):
+                raise ValueError(f"wind_index: values must index the env's {len(self._winds)} wind matrices")
             put(self.wind_index, wind_index, torch.int32)
         if dousing is not None:
             put(self.dousing, dousing, torch.uint8)

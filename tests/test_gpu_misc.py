@@ -89,6 +89,8 @@ def test_positions_outside_the_grid_write_nothing(device):
     obs, info = adv.reset()
     with pytest.raises(ValueError):
         adv.set_state(position=[[0, 0], [3, 16]])
+    with pytest.raises(ValueError):
+        adv.set_state(wind_index=[0, len(adv._winds)])
     adv.stateless_step(torch.zeros((2, 3), dtype=torch.int32, device=device), obs, info)  # the valid call runs
     bad = dict(obs[1])
     bad["position"] = torch.tensor([[0, 0], [16, 1]], dtype=torch.int32, device=device)
