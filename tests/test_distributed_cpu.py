@@ -189,6 +189,26 @@ def test_bench_torchrun_launch_measures_the_cpu_baseline_on_rank0():
     _check_cpu_legs(out, "rank 0")
 
 
+def test_bench_torchrun_eight_ranks_rehearsal():
+    """The driver's 8-GPU launch shape (torch.distributed.run --nproc-per-node 8 in front of bench.py --gpus 8) on gloo:
+    8 ranks of 5 envs each (weak scaling: --envs is per rank), the episode-stats all-gather in rank order."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    e = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "GCA_BENCH_CPU_JSON")}
+    e["OMP_NUM_THREADS"] = "1"
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=8",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"),
+                        "--gpus", "8", "--dry-run", "--envs", "5", "--no-cpu-baseline"],
+                       capture_output=True, text=True, timeout=240, env=e, cwd=root)
+    assert p.returncode == 0, p.stderr[-2000:]
+    out = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert out["n_gpus"] == 8 and out["gather_ok"]
+    assert [(r["rank"], r["env_offset"], r["envs"]) for r in out["ranks"]] == [(k, 5 * k, 5) for k in range(8)]
+
+
 def test_bench_refuses_a_world_size_mismatch():
     rc, out, err = _bench("--gpus", "2", env={"WORLD_SIZE": "1", "RANK": "0"})
     assert rc != 0 and out is None and "WORLD_SIZE=1" in err
