@@ -2,9 +2,12 @@
 as written — neighbourhood tensors, weighted sums, f32 arithmetic — in numpy, with the
 random arrays injected. Test infrastructure only.
 
-jax is not installed, so this cannot be checked against the reference executing; it is
-pinned by line-for-line restatement, the reference's invariants (tests/test_alexandridis_*)
-and `burn_probability_f64`, an independent float64 evaluation of the probability formula.
+Pinned (r06) to the reference EXECUTING: tests/golden/alexandridis_jax.npz holds consecutive `update`
+calls of ca_alexandridis_jax.py run as published under a numpy stand-in for jnp / jit / vmap / lax /
+random (tests/golden/_jax_standin.py; jax itself is not installed), with every random array the rule
+consumed and the burn probabilities it computed; tests/test_alexandridis_jax_golden.py checks this
+restatement and the C oracle against it. Also checked against `burn_probability_f64`, an independent
+float64 evaluation of the probability formula.
 """
 import math
 
@@ -72,6 +75,11 @@ def burn_probability_f64(grid, veg, den, wind, slope, dousing, C, fire=2):
     p_den = DEN.astype(np.float64)[np.clip(den, 1, 5)]
     return ((heat - dous)[..., None, None] * (1 + p_veg)[..., None, None] * (1 + p_den)[..., None, None]
             * np.asarray(wind, np.float64) * np.exp(0.078 * np.asarray(slope, np.float32).astype(np.float64)))
+
+
+def wind_change(wind_index, n_winds, p_wind_change, u, k):
+    """update's wind change (:443-451) with the injected uniform u and offset k in [1, 8)."""
+    return (int(wind_index) + int(k)) % int(n_winds) if np.float32(u) < np.float32(p_wind_change) else int(wind_index)
 
 
 def update_grid(grid, fire_age, veg, den, slope, dousing, wind, p_tree, u_burn, u_grow, new_ages, C,

@@ -488,17 +488,120 @@ def gen_alexandridis_classic(R, rng):
     return out
 
 
+# (grid_size, H, W, steps, fire_frac, hidden slope from altitude, p_tree, p_wind_change, burn-draw scale: the burn
+#  uniforms are drawn on [0, scale) so that ignitions are frequent at these small probabilities)
+ALEX_JAX_CASES = [(256, 16, 256, 3, 0.10, True, 0.05, 0.5, 0.03),   # configs 3/4: R = 6, ages [576, 672)
+                  (512, 16, 512, 2, 0.10, True, 0.05, 0.5, 0.03),   # config 5's grid: R = 7, ages [1152, 1344)
+                  (256, 20, 24, 4, 0.25, False, 0.10, 0.9, 0.05),   # ragged small grid, free slopes, hot draws
+                  (64, 48, 48, 3, 0.15, True, 0.0, 0.06, 0.1)]      # R = 4, the env's p_tree / p_wind_change
+
+
+def gen_alexandridis_jax(R, rng):
+    """PartiallyObservableForestFireJax (ca_alexandridis_jax.py:54-160 constructor, :164-206 burn probability,
+    :321-424 _update_grid, :426-460 update) EXECUTED as published, under tests/golden/_jax_standin.py's numpy
+    stand-in for jnp / jit / vmap / lax / random. Several consecutive `update` calls per case, the reference's
+    returned per_env_context fed back. Recorded per step: the inputs, every random array in call order (burn
+    uniforms (H,W,3,3), grow uniforms (H,W), new fire ages (H,W), wind-change uniform, wind offset), the
+    burn probabilities _compute_burn_probability returned, and the outputs (grid, fire_age, wind_index).
+    Winds from the reference's get_winds(True) (init_utils.py:233-245); slopes from its get_slope of its
+    init_altitude (:76-116, :166-200) where `hidden`, else free normal(0, 20) slopes (not antisymmetric)."""
+    import contextlib
+    import io
+
+    sys.path.insert(0, HERE)
+    import _jax_standin as js
+
+    rlog = js.RandomLog(np.random.default_rng(0))
+    with js.installed(rlog):
+        iu = _load("gym_cellular_automata.forest_fire.bulldozer.utils.init_utils",
+                   f"{REF}/forest_fire/bulldozer/utils/init_utils.py")
+        aj = _load("gym_cellular_automata.forest_fire.operators.ca_alexandridis_jax",
+                   f"{REF}/forest_fire/operators/ca_alexandridis_jax.py")
+    cls = aj.PartiallyObservableForestFireJax
+    captured = []
+    orig_bp = cls._compute_burn_probability
+
+    def bp(self, *a):
+        r = orig_bp(self, *a)
+        captured.append(np.asarray(r).copy())
+        return r
+
+    cls._compute_burn_probability = bp
+    winds = np.asarray(iu.get_winds(True), dtype=np.float64)  # (8, 2, 3, 3), jnp.array -> float32 below
+    out = {"winds": winds.astype(np.float32)}
+    try:
+        for ci, (gs, H, W, steps, ff, hidden, p_tree, p_wc, bscale) in enumerate(ALEX_JAX_CASES):
+            crng = np.random.default_rng(4242 + ci)
+            grid = crng.choice([0, 1, 2], size=(H, W), p=[0.1, 0.9 - ff, ff])
+            fire_age = np.where(crng.random((H, W)) < 0.3, crng.integers(-1, 3, (H, W)),  # burn-outs (age <= 1)
+                                crng.integers(1, int(gs * 1.5 * 1.75) + 1, (H, W)))
+            age = np.where(grid == 2, fire_age, crng.integers(-2, 3, (H, W))).astype(np.float32)
+            veg = crng.integers(0, 7, (H, W))  # 0 and 6 exercise the reference's clip to 1..5 (:176-178)
+            den = crng.integers(0, 7, (H, W))
+            dous = (crng.random((H, W)) < 0.08).astype(np.int32)
+            if hidden:
+                np.random.seed(900 + ci)
+                alt = iu.init_altitude(H, W, 1)
+                with contextlib.redirect_stdout(io.StringIO()):  # get_slope prints a histogram
+                    slope = np.asarray(iu.get_slope(alt, H, W, 1))[0]
+                out[f"c{ci}_altitude"] = alt[0]
+            else:
+                slope = crng.normal(0, 20, (H, W, 3, 3)).clip(-89, 89)
+                slope[..., 1, 1] = 0
+            wrap = js.wrap
+            with js.installed(rlog):
+                op = cls(gs, 0, 1, 2)
+            shared = {"winds": wrap(winds), "p_tree": wrap(np.float32(p_tree)),
+                      "p_wind_change": wrap(np.float32(p_wc))}
+            ctx = {"wind_index": wrap(np.int32(crng.integers(0, 8))), "density": wrap(den),
+                   "vegetation": wrap(veg), "slope": wrap(slope), "fire_age": wrap(age),
+                   "dousing_count": wrap(dous), "key": ("key", -1)}
+            g = wrap(grid)
+            out[f"c{ci}_meta"] = np.array([gs, H, W, steps])
+            out[f"c{ci}_p"] = np.array([p_tree, p_wc], dtype=np.float32)
+            out[f"c{ci}_veg"], out[f"c{ci}_den"] = veg.astype(np.uint8), den.astype(np.uint8)
+            out[f"c{ci}_dous"] = dous.astype(np.uint8)
+            out[f"c{ci}_slope"] = np.asarray(ctx["slope"])  # float32 (jax canonicalises float64 inputs)
+            rlog.gen = np.random.default_rng(7000 + ci)
+            rlog.uniform_scale = lambda shape, bscale=bscale: bscale if len(shape) == 4 else 1.0
+            for t in range(steps):
+                rlog.log.clear()
+                captured.clear()
+                pre = f"c{ci}_s{t}_"
+                out[pre + "grid"] = np.asarray(g).astype(np.uint8)
+                out[pre + "age"] = np.asarray(ctx["fire_age"]).astype(np.float32)
+                out[pre + "wind"] = np.array(int(ctx["wind_index"]))
+                g, ctx, _ = op.update(g, None, ctx, shared)
+                kinds = [(k, len(s)) for k, s, _, _ in rlog.log]
+                assert kinds == [("uniform", 4), ("uniform", 2), ("randint", 2), ("uniform", 0), ("randint", 0)], kinds
+                assert rlog.log[2][3] == (int(op.fire_age_min), int(op.fire_age_max)) and rlog.log[4][3] == (1, 8)
+                assert len(captured) == 1 and captured[0].dtype == np.float32, "jax's f32 arithmetic was not kept"
+                out.update({pre + "u_burn": rlog.log[0][2], pre + "u_grow": rlog.log[1][2],
+                            pre + "new_ages": rlog.log[2][2], pre + "wind_u": np.float32(rlog.log[3][2]),
+                            pre + "wind_k": np.int32(rlog.log[4][2]), pre + "probs": captured[0],
+                            pre + "out_grid": np.asarray(g).astype(np.uint8),
+                            pre + "out_age": np.asarray(ctx["fire_age"]).astype(np.float32),
+                            pre + "out_wind": np.array(int(ctx["wind_index"]))})
+                assert np.asarray(ctx["fire_age"]).dtype == np.float32
+    finally:
+        cls._compute_burn_probability = orig_bp
+    out["n"] = np.array(len(ALEX_JAX_CASES))
+    return out
+
+
 GENERATORS = {"windy": gen_windy, "repeat_ca": gen_repeat, "move_modify": gen_move_modify, "bulldozer": gen_bulldozer,
               "drossel": gen_drossel, "helicopter": gen_helicopter, "moore": gen_moore, "init_utils": gen_init_utils,
-              "alexandridis_classic": gen_alexandridis_classic}
+              "alexandridis_classic": gen_alexandridis_classic, "alexandridis_jax": gen_alexandridis_jax}
 
 
 def main():
     R = load_reference()
     rng = np.random.default_rng(20260101)
     names = sys.argv[1:] or list(GENERATORS)
-    for name, fn in GENERATORS.items():
-        data = fn(R, rng)  # every generator runs, in order, so the shared rng stream is unchanged
+    order = list(GENERATORS)
+    last = max(order.index(n) for n in names)
+    for name in order[:last + 1]:
+        data = GENERATORS[name](R, rng)  # every earlier generator runs, in order, so the shared rng stream is unchanged
         if name not in names:
             continue
         path = os.path.join(HERE, f"{name}.npz")
