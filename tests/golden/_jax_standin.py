@@ -8,10 +8,11 @@ fixtures it yields come from the reference running, not from a restatement:
           (float64 -> float32, int64 -> int32), float literals / jnp.array / jnp.zeros default to float32,
           an integer or bool array meeting a float array is converted to that float type BEFORE the
           operation (jax's promotion lattice: int32 * float32 -> float32, where numpy would give float64),
-          python scalars are weakly typed; `.at[idx].set(v)` is the functional update
+          python scalars are weakly typed; `.at[idx].set(v)` is the functional update; out-of-bounds integer
+          indices are clamped (jax's gather) instead of raising; `x += y` rebinds (jax arrays are immutable)
   jit     identity (also `partial(jit, static_argnums=...)`)
   vmap    an explicit loop over `in_axes` (tuples of arrays map leaf-wise), results stacked on axis 0
-  lax     dynamic_slice as a slice (start indices clamped like lax does)
+  lax     dynamic_slice as a slice (start indices clamped like lax does), switch (index clamped)
   random  keys are opaque tokens; every draw (uniform / randint / normal / poisson) comes from a numpy
           Generator and is logged in call order, so a fixture can inject the very arrays the rule consumed.
           randint truncates non-integer bounds to int first, like jax.random.randint (minval.astype(int)).
@@ -21,6 +22,7 @@ numpy's order here (pairwise), and exp is numpy's float32 exp. Both differ from 
 two, which is why the parity tests hold probabilities to 1e-6 and integer states to equality except where a
 uniform draw lies within 1e-6 of its probability.
 """
+import dataclasses
 import sys
 import types
 from contextlib import contextmanager
@@ -67,6 +69,58 @@ class JArray(np.ndarray):
     @property
     def at(self):
         return _At(self)
+
+    def __getitem__(self, idx):
+        return super().__getitem__(_clamp_index(self.shape, idx))
+
+    def __iter__(self):  # iteration stops at the end (indexing itself clamps and would never raise)
+        sup = super().__getitem__
+        return (sup(i) for i in range(len(self)))
+
+    # jax arrays are immutable: `x += y` rebinds x to a new array
+    def __iadd__(self, o):
+        return self + o
+
+    def __isub__(self, o):
+        return self - o
+
+    def __imul__(self, o):
+        return self * o
+
+    def __itruediv__(self, o):
+        return self / o
+
+
+def _clamp_index(shape, idx):
+    """jnp indexing: integer indices (scalars or arrays) are normalised (negative from the end) and then CLAMPED
+    to the axis, as jax's gather does out of bounds, instead of raising like numpy."""
+    if not isinstance(idx, tuple):
+        idx = (idx,)
+    n_used = sum(0 if (i is None or i is Ellipsis) else (np.ndim(i) if _is_bool(i) else 1) for i in idx)
+    out, ax = [], 0
+    for i in idx:
+        if i is None:
+            out.append(i)
+        elif i is Ellipsis:
+            out.append(i)
+            ax += len(shape) - n_used
+        elif isinstance(i, slice) or _is_bool(i):
+            out.append(i.view(np.ndarray) if isinstance(i, JArray) else i)
+            ax += np.ndim(i) if _is_bool(i) else 1
+        elif isinstance(i, (int, np.integer)) or (isinstance(i, np.ndarray) and np.issubdtype(i.dtype, np.integer)):
+            d = shape[ax]
+            v = np.asarray(i).view(np.ndarray)
+            v = np.clip(np.where(v < 0, v + d, v), 0, d - 1)
+            out.append(int(v) if v.ndim == 0 else v)
+            ax += 1
+        else:
+            out.append(i)
+            ax += 1
+    return tuple(out)
+
+
+def _is_bool(i):
+    return isinstance(i, np.ndarray) and i.dtype == np.bool_
 
 
 class _At:
@@ -172,6 +226,8 @@ def _make_jnp():
 
     def pad(a, pad_width, mode="constant", constant_values=0):
         a = np.asarray(a)
+        if mode != "constant":
+            return wrap(np.pad(a, pad_width, mode=mode))
         return wrap(np.pad(a, pad_width, mode=mode, constant_values=np.asarray(constant_values).astype(a.dtype)))
 
     def arange(*a, dtype=None):
@@ -264,7 +320,10 @@ def _make_lax():
         st = [int(min(max(int(s), 0), d - z)) for s, d, z in zip(start, a.shape, sizes)]  # lax clamps starts
         return wrap(a[tuple(slice(s, s + z) for s, z in zip(st, sizes))])
 
-    lax.dynamic_slice = dynamic_slice
+    def switch(index, branches, *operands):
+        return branches[int(np.clip(int(index), 0, len(branches) - 1))](*operands)  # lax.switch clamps the index
+
+    lax.dynamic_slice, lax.switch = dynamic_slice, switch
     return lax
 
 
@@ -325,7 +384,8 @@ def installed(rlog):
     jax.numpy, jax.lax, jax.random, jax.jit, jax.vmap = jnp, lax, rnd, jit, vmap
     jax.debug = types.SimpleNamespace(callback=lambda *a, **k: None, print=lambda *a, **k: None)
     flax = types.ModuleType("flax")
-    flax.struct = types.SimpleNamespace(dataclass=lambda c=None, **k: c if c is not None else (lambda x: x))
+    flax.struct = types.SimpleNamespace(dataclass=lambda c=None, **k: dataclasses.dataclass(frozen=True)(c)
+                                        if c is not None else dataclasses.dataclass(frozen=True))
     names = ("jax", "jax.numpy", "jax.lax", "jax.random", "flax", "flax.struct")
     saved = {k: sys.modules.get(k) for k in names}
     sys.modules.update({"jax": jax, "jax.numpy": jnp, "jax.lax": lax, "jax.random": rnd, "flax": flax,

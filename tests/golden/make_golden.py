@@ -589,9 +589,79 @@ def gen_alexandridis_jax(R, rng):
     return out
 
 
+def _load_advanced_mdp(js, rlog):
+    """advanced_bulldozer.py's MDP class, loaded under the jax stand-in. The module's other imports get what
+    they need to import: the operator classes (unused by the observation builders) as placeholders, an empty
+    render module; extension_utils.py and init_utils.py are the reference's own files."""
+    ops = sys.modules["gym_cellular_automata.forest_fire.operators"]
+    for name in ("ModifyJax", "MoveJax", "MoveModifyJax", "RepeatCAJax", "PartiallyObservableForestFireJax"):
+        if not hasattr(ops, name):
+            setattr(ops, name, type(name, (), {}))
+    r = types.ModuleType("gym_cellular_automata.forest_fire.bulldozer.utils.advanced_bulldozer_render")
+    r.render, r.plot_grid_attribute = (lambda *a, **k: None), (lambda *a, **k: None)
+    sys.modules[r.__name__] = r
+    with js.installed(rlog):
+        _load("gym_cellular_automata.forest_fire.bulldozer.utils.init_utils",
+              f"{REF}/forest_fire/bulldozer/utils/init_utils.py")
+        eu = _load("gym_cellular_automata.forest_fire.bulldozer.utils.extension_utils",
+                   f"{REF}/forest_fire/bulldozer/utils/extension_utils.py")
+        ab = _load("gym_cellular_automata.forest_fire.bulldozer.advanced_bulldozer",
+                   f"{REF}/forest_fire/bulldozer/advanced_bulldozer.py")
+    return ab, eu
+
+
+def gen_observation(R, rng):
+    """The Advanced env's observation builders EXECUTED as published under the jax stand-in:
+    MDP.build_observation_on_extensions (advanced_bulldozer.py:988-1018: transform_grid / apply_extensions of
+    extension_utils.py:89-196, then grid_to_rgb_with_extensions :1020-1033 and grid_to_rgb :1035-1101) for the
+    step frame, and grid_to_rgb_with_extensions on a plain (H, W) grid for the reset frame (:401-411 applies it
+    per env; oracle/observation.reset_observation's convention; square grids only — on a non-square grid those
+    expressions do not broadcast, in jax as in numpy). Inputs: grids of codes 0/1/2 (one case also 3,
+    the code apply_visibility hides), dousing counts 0..2 (the water tint only at 1, :1081), day / night, the
+    position on the border and inside, extension flags of the action (actions[2:]), enable_extensions and
+    should_transform_grid on / off."""
+    sys.path.insert(0, HERE)
+    import _jax_standin as js
+
+    rlog = js.RandomLog(np.random.default_rng(0))
+    ab, _ = _load_advanced_mdp(js, rlog)
+    wrap = js.wrap
+    crng = np.random.default_rng(5150)
+    out = {}
+    cases = [(5, 5), (8, 8), (17, 23), (64, 64), (1, 6), (32, 16)]
+    n = 0
+    for H, W in cases:
+        for k in range(6):
+            codes = [0, 1, 2, 3] if (H, W) == (17, 23) and k < 3 else [0, 1, 2]
+            grid = crng.choice(codes, size=(H, W), p=None).astype(np.float32)
+            dous = crng.choice([0, 1, 2], size=(H, W), p=[0.7, 0.2, 0.1]).astype(np.int32)
+            pos = np.array([crng.integers(0, H), crng.integers(0, W)] if k % 2 else [0, W - 1], np.int32)
+            night = np.int32(k % 2 if k < 4 else crng.integers(0, 2))
+            flags = [(0, 0), (1, 0), (0, 1), (1, 1)][crng.integers(0, 4)]
+            enable, transform = bool(crng.integers(0, 2)), bool(crng.integers(0, 2))
+            actions = np.array([crng.integers(0, 9), crng.integers(0, 2), *flags], np.int32)
+            mdp = ab.MDP.__new__(ab.MDP)
+            mdp.tree, mdp.fire, mdp.empty = 1, 2, 0
+            mdp.should_transform_grid, mdp.enable_extensions = transform, enable
+            ctx = {"is_night": wrap(night), "dousing_count": wrap(dous)}
+            rgb, ch = mdp.build_observation_on_extensions(wrap(grid), wrap(pos), wrap(actions), ctx, {})
+            # the reset convention broadcasts (H, 3) against (H, W, 1): defined for square grids only
+            reset = mdp.grid_to_rgb_with_extensions(wrap(grid), ctx, wrap(pos)) if H == W else np.zeros(0)
+            pre = f"c{n}_"
+            out.update({pre + "grid": grid.astype(np.uint8), pre + "dous": dous.astype(np.uint8), pre + "pos": pos,
+                        pre + "night": np.array(int(night)), pre + "actions": actions,
+                        pre + "flags": np.array([int(enable), int(transform)]),
+                        pre + "rgb": np.asarray(rgb), pre + "channels": np.asarray(ch), pre + "reset": np.asarray(reset)})
+            assert np.asarray(rgb).dtype == np.float32 and np.asarray(rgb).shape == (H, W, 3)
+            n += 1
+    out["n"] = np.array(n)
+    return out
+
+
 GENERATORS = {"windy": gen_windy, "repeat_ca": gen_repeat, "move_modify": gen_move_modify, "bulldozer": gen_bulldozer,
               "drossel": gen_drossel, "helicopter": gen_helicopter, "moore": gen_moore, "init_utils": gen_init_utils,
-              "alexandridis_classic": gen_alexandridis_classic, "alexandridis_jax": gen_alexandridis_jax}
+              "alexandridis_classic": gen_alexandridis_classic, "alexandridis_jax": gen_alexandridis_jax,
+              "observation": gen_observation}
 
 
 def main():

@@ -236,3 +236,33 @@ def test_fused_frames_equal_the_observation_pass_at_config3(device, enable):
         assert not bool(diff.any()), (s, torch.nonzero(diff)[:5].flatten().tolist())
     if enable:
         assert 0 < int(env._refit.sum()) < E  # both the epilogue's frames and refits
+
+
+def test_observation_kernel_reproduces_reference_run(device, golden):
+    """gca_adv_observation against the reference's own observation builders executed
+    (tests/golden/observation.npz, see tests/test_observation_golden.py): every case whose extension flags the
+    env's action space can express (EXTENSION_LOOKUP: choose = 1), the step frame and channels bit for bit, and the
+    reset frame on square grids."""
+    from gymca_amd.forest_fire.bulldozer.observation import EXTENSION_LOOKUP, make_obs_params
+
+    d = golden("observation")
+    lookup = [tuple(int(b) for b in row) for row in EXTENSION_LOOKUP]
+    checked = 0
+    for i in range(int(d["n"])):
+        p = f"c{i}_"
+        a = d[p + "actions"]
+        if tuple(int(v) for v in a[2:]) not in lookup:
+            continue
+        enable, transform = (bool(v) for v in d[p + "flags"])
+        grid, dous = d[p + "grid"][None], d[p + "dous"][None]
+        pos, night = d[p + "pos"][None], np.array([int(d[p + "night"])])
+        action = np.array([[a[0], a[1], lookup.index(tuple(int(v) for v in a[2:]))]])
+        params = make_obs_params(0, 1, 2, enable, transform, 400)
+        rgb, ch = run(device, params, 0, grid, dous, pos, night, np.array([1]), action, channels=True)
+        assert np.array_equal(rgb[0], d[p + "rgb"]), i
+        assert np.array_equal(ch[0], d[p + "channels"].astype(np.uint8)), i
+        if d[p + "reset"].size:
+            rgb0, _ = run(device, params, 1, grid, dous, pos, night)
+            assert np.array_equal(rgb0[0], d[p + "reset"]), i
+        checked += 1
+    assert checked >= 20
