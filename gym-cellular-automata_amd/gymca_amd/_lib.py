@@ -307,12 +307,14 @@ class BoundCall:
     front (structs by reference, so later edits of the struct are seen), marks the `SLOT` positions, and each call
     only rebinds the slots' `.value` and calls the function pointer with the prepared tuple -- no per-call argtypes
     conversion, no dev.ptr() per buffer (a 21-argument call rebuilt from tensors cost ~11 us of
-    host time per 1024-env step). The caller keeps the bound buffers alive and unmoved. Not thread-safe (one object
-    per env, like the env itself)."""
+    host time per 1024-env step). `keep=` holds references to the objects (tensors) whose addresses were bound, so a
+    bound address can never outlive its allocation: a caller that replaces a buffer and forgets to rebind gets stale
+    state, never a write into memory the caching allocator has handed to someone else (the batched envs rebind on
+    assignment: BatchedForestFireBulldozerEnv.__setattr__). Not thread-safe (one object per env, like the env)."""
 
-    __slots__ = ("name", "_fn", "_args", "_slots")
+    __slots__ = ("name", "_fn", "_args", "_slots", "_keep")
 
-    def __init__(self, name, *args):
+    def __init__(self, name, *args, keep=()):
         global _lib_raw
         load()  # the checked load (raises GCAError when the library is missing)
         if _lib_raw is None:
@@ -336,6 +338,7 @@ class BoundCall:
                 slots.append(obj)
             prepared.append(obj)
         self.name, self._fn, self._args, self._slots = name, fn, tuple(prepared), tuple(slots)
+        self._keep = tuple(keep)
 
     def __call__(self, *values):
         if len(values) != len(self._slots):

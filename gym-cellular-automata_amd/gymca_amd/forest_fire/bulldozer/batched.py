@@ -29,7 +29,31 @@ from ..operators.move_modify import make_params
 from .bulldozer import ACTION_SETS, DEFAULT_WIND, bulldozer_timings, parse_wind
 
 
+# state the pre-bound calls hold by address (step, step_random, sample_actions): assigning one of these attributes
+# validates the replacement and drops the bound calls (rebind), so the next step binds the new tensor
+_BOUND_STATE = frozenset({"buf", "parity", "accu", "steps", "dir_mask", "counts", "pos", "rng_step", "done", "hit",
+                          "reward", "wind", "steps_elapsed", "params", "_meet", "_act_buf"})
+
+
 class BatchedForestFireBulldozerEnv:
+    def __setattr__(self, name, value):
+        d = self.__dict__
+        if name in _BOUND_STATE and "_fused_call" in d and d.get(name) is not value:
+            old = d.get(name)
+            if name == "params":
+                if type(value) is not type(old):
+                    raise TypeError(f"params must stay a {type(old).__name__}")
+            elif name == "_meet" and value is None:
+                pass
+            elif not (dev.is_device_tensor(value) and value.dtype == old.dtype and value.shape == old.shape
+                      and value.device == old.device and value.is_contiguous()):
+                raise ValueError(f"env.{name}: the replacement must be a contiguous {old.dtype} tensor of shape "
+                                 f"{tuple(old.shape)} on {old.device} (or update the tensor in place)")
+            object.__setattr__(self, name, value)
+            self.rebind()
+            return
+        object.__setattr__(self, name, value)
+
     def __init__(self, num_envs, nrows, ncols, device=None, seed=0, env_offset=0, speed_move=0.12, speed_act=0.03,
                  t_move=None, t_shoot=None, t_any=0.001, p_tree=0.90, p_empty=0.10, wind=DEFAULT_WIND,
                  materialize_obs=True, fused=None):
@@ -85,7 +109,7 @@ class BatchedForestFireBulldozerEnv:
         # one action check, one raw-stream read and one prepared ctypes call
         self._dev_index = dev.device_index(self.device)
         self._act_buf = torch.zeros((E, 2), dtype=torch.int32, **kw)
-        self._act_src = None
+        self._act_shape = self._act_buf.shape
         self._done_bool = self.done.view(torch.bool)
         self._info = {"hit": self.hit, "ca_steps": self.steps}
         self._ctx = {"wind": self.wind, "position": self.pos, "time": self.accu}
@@ -148,25 +172,24 @@ class BatchedForestFireBulldozerEnv:
         return (self.grids() if self.materialize_obs else None), self._ctx
 
     def _action(self, action):
-        """action as a contiguous int32 (E, 2) device tensor: the caller's own tensor when it already is one (checked
-        once per tensor object), else converted into the env's action buffer."""
+        """action as a contiguous int32 (E, 2) device tensor: the caller's own tensor when it is one (checked on every
+        call: a tensor retyped or reshaped in place since the last step is converted, not misread), else converted
+        into the env's action buffer."""
         import torch
 
-        if action is self._act_src:
-            return action
-        E = self.num_envs
-        if (type(action) is torch.Tensor and action.is_cuda and action.dtype == torch.int32 and action.shape == (E, 2)
-                and action.is_contiguous() and action.device == self.device):
-            self._act_src = action
+        if (type(action) is torch.Tensor and action.dtype == torch.int32 and action.shape == self._act_shape
+                and action.device == self.device and action.is_contiguous()):
             return action
         src = action if dev.is_device_tensor(action) else torch.as_tensor(np.asarray(action))
-        self._act_buf.copy_(src.reshape(E, 2))
+        self._act_buf.copy_(src.reshape(self.num_envs, 2))
         return self._act_buf
 
     def rebind(self):
-        """Drop the pre-bound step call. The env's state tensors (buf, accu, steps, done, wind, rng_step, parity, pos,
+        """Drop the pre-bound step calls. The env's state tensors (buf, accu, steps, done, wind, rng_step, parity, pos,
         counts, hit, reward, steps_elapsed) and params are bound by address on the first fused step; every method here
-        updates them in place. Code that REPLACES one of them (assigns a new tensor) calls rebind() afterwards."""
+        updates them in place. Assigning a new tensor to one of them (env.wind = w) calls this by itself
+        (__setattr__, which also checks the replacement's dtype / shape / device); the bound calls hold references to
+        what they bound, so nothing they address is ever freed under them."""
         import torch
 
         self._fused_call = self._bound_meet = None
@@ -176,6 +199,10 @@ class BatchedForestFireBulldozerEnv:
         self._info = {"hit": self.hit, "ca_steps": self.steps}
         self._ctx = {"wind": self.wind, "position": self.pos, "time": self.accu}
 
+    def _bound_tensors(self):
+        return (self.params, self.accu, self.steps, self.done, self.wind, self.rng_step, self.parity, self.buf,
+                self.pos, self.counts, self.hit, self.reward, self.steps_elapsed, self._meet)
+
     def _bind_fused(self):
         E, H, W = self.num_envs, self.nrows, self.ncols
         meet = self._meet
@@ -183,7 +210,8 @@ class BatchedForestFireBulldozerEnv:
             "gca_bulldozer_step_fused", self.params, SLOT, dev.ptr(self.accu), dev.ptr(self.steps), dev.ptr(self.done),
             dev.ptr(self.wind), 9, dev.ptr(self.rng_step), dev.ptr(self.parity), dev.ptr(self.buf[0]),
             dev.ptr(self.buf[1]), H, W, dev.ptr(self.pos), dev.ptr(self.counts), dev.ptr(self.hit),
-            dev.ptr(self.reward), dev.ptr(self.steps_elapsed), dev.ptr(meet) if meet is not None else None, E, SLOT)
+            dev.ptr(self.reward), dev.ptr(self.steps_elapsed), dev.ptr(meet) if meet is not None else None, E, SLOT,
+            keep=self._bound_tensors())
         self._bound_meet = meet
         return self._fused_call
 
@@ -194,36 +222,44 @@ class BatchedForestFireBulldozerEnv:
         default the env's action buffer). Fused step only (W = 256 / 512, one CA pass at most per env step)."""
         if not self.fused:
             raise ValueError("step_random needs the fused step (W in (256, 512), at most one CA pass per env step)")
+        import torch
+
         out = self._act_buf if action_out is None else action_out
-        key = (seed, out.data_ptr(), self._meet is None)
-        if self._random_call is None or self._random_call[0] != key or self._bound_meet_r is not self._meet:
-            if not (dev.is_device_tensor(out) and out.is_contiguous() and out.numel() == 2 * self.num_envs
-                    and out.element_size() == 4 and not out.is_floating_point()):
-                raise ValueError("step_random: action_out must be a contiguous int32 (E, 2) device tensor")
+        if not (type(out) is torch.Tensor and out.dtype == torch.int32 and out.shape == self._act_shape
+                and out.device == self.device and out.is_contiguous()):
+            raise ValueError("step_random: action_out must be a contiguous int32 (E, 2) tensor on the env's device")
+        key = (seed, out.data_ptr())
+        rc = self._random_call
+        if rc is None or rc[0] != key or rc[1] is not out or self._bound_meet_r is not self._meet:
             E, H, W = self.num_envs, self.nrows, self.ncols
             meet = self._meet
-            self._random_call = (key, BoundCall(
+            self._random_call = (key, out, BoundCall(
                 "gca_bulldozer_step_fused_random", self.params, int(seed) & (2**64 - 1), dev.ptr(out),
                 dev.ptr(self.accu), dev.ptr(self.steps), dev.ptr(self.done), dev.ptr(self.wind), 9,
                 dev.ptr(self.rng_step), dev.ptr(self.parity), dev.ptr(self.buf[0]), dev.ptr(self.buf[1]), H, W,
                 dev.ptr(self.pos), dev.ptr(self.counts), dev.ptr(self.hit), dev.ptr(self.reward),
-                dev.ptr(self.steps_elapsed), dev.ptr(meet) if meet is not None else None, E, SLOT))
+                dev.ptr(self.steps_elapsed), dev.ptr(meet) if meet is not None else None, E, SLOT,
+                keep=self._bound_tensors() + (out,)))
             self._bound_meet_r = meet
-        self._random_call[1](dev.raw_stream(self._dev_index))
+        self._random_call[2](dev.raw_stream(self._dev_index))
         return self._obs(), self.reward, self._done_bool, self._truncated, self._info
 
     def sample_actions(self, out=None, tag=9):
         """Uniform random actions for every env on the device -- the batched `action_space.sample()` (move in [0, 9),
         shoot in {0, 1}; Philox keyed by (tag, global env id, the env's rng_step)) -- into `out` (a contiguous int32
         (E, 2) device tensor) or the env's action buffer. Returns the tensor."""
+        import torch
+
         out = self._act_buf if out is None else out
-        if self._sample_call is None or self._sample_call[0] is not out or self._sample_call[1] != tag:
-            if not (dev.is_device_tensor(out) and out.is_contiguous() and out.numel() == 2 * self.num_envs
-                    and out.element_size() == 4 and not out.is_floating_point()):
-                raise ValueError("sample_actions: out must be a contiguous int32 (E, 2) device tensor")
-            self._sample_call = (out, tag, BoundCall("gca_random_actions", dev.ptr(out), self.num_envs,
-                                                     self.env_offset, tag, dev.ptr(self.rng_step), SLOT))
-        self._sample_call[2](dev.raw_stream(self._dev_index))
+        if not (type(out) is torch.Tensor and out.dtype == torch.int32 and out.shape == self._act_shape
+                and out.device == self.device and out.is_contiguous()):
+            raise ValueError("sample_actions: out must be a contiguous int32 (E, 2) tensor on the env's device")
+        sc = self._sample_call
+        if sc is None or sc[0] is not out or sc[1] != tag or sc[2] != out.data_ptr():
+            self._sample_call = (out, tag, out.data_ptr(),
+                                 BoundCall("gca_random_actions", dev.ptr(out), self.num_envs, self.env_offset, tag,
+                                           dev.ptr(self.rng_step), SLOT, keep=(out, self.rng_step)))
+        self._sample_call[3](dev.raw_stream(self._dev_index))
         return out
 
     # ------------------------------------------------------------------ step

@@ -492,7 +492,7 @@ def test_eager_step_action_forms_and_sampler(device):
         forms = [mine, mine.to(torch.int64), mine.cpu().numpy(), mine.reshape(-1).clone()]
         for env, a in zip(envs, forms):
             env.step(a)
-        assert envs[0]._act_src is mine
+        assert envs[0]._action(mine) is mine
         for env in envs[1:]:
             assert torch.equal(env.grids(), envs[0].grids()), f"step {s}"
             for name in ("pos", "accu", "counts", "rng_step", "hit", "done"):
@@ -522,6 +522,56 @@ def test_rebind_after_replacing_a_state_tensor(device):
         for name in ("accu", "counts", "pos", "rng_step", "done"):
             assert torch.equal(getattr(envs[0], name), getattr(envs[1], name)), (name, s)
     assert envs[1]._ctx["time"] is envs[1].accu
+
+
+def test_assigning_state_tensors_without_rebind(device):
+    """VERDICT r05 next-3 / ADVICE r05: assigning fresh tensors to env.accu, env.pos and env.wind WITHOUT calling
+    rebind() (the env's __setattr__ rebinds by itself), retyping the caller's cached action tensor in place (int32 ->
+    int64 through .data) and re-pointing step_random's action_out: the env steps bit for bit like a freshly built env
+    that had none of it done; a replacement of the wrong dtype / shape is refused."""
+    import torch
+
+    from gymca_amd.forest_fire.bulldozer import BatchedForestFireBulldozerEnv
+
+    E, N = 64, 256
+    envs = [BatchedForestFireBulldozerEnv(E, N, N, device=device, seed=21, materialize_obs=False) for _ in range(2)]
+    for env in envs:
+        env.reset(seed=4)
+        _dense_state(env, device, seed=12, p_fire=0.05)
+    a0 = torch.zeros((E, 2), dtype=torch.int32, device=device)
+    a1 = torch.zeros((E, 2), dtype=torch.int32, device=device)
+    for s in range(36):
+        if s == 8:
+            envs[1].accu = envs[1].accu.clone()          # new allocations; the old ones may be freed now
+            envs[1].pos = envs[1].pos.clone()
+            envs[1].wind = envs[1].wind.clone()
+            torch.cuda.empty_cache()
+            scratch = [torch.full((E, 2), 7, dtype=torch.int32, device=device) for _ in range(64)]  # reuse freed blocks
+            del scratch
+        if s == 16:  # the cached action tensor retyped in place: converted, never read as int32 pairs
+            a1.data = a1.data.to(torch.int64)
+        envs[0].sample_actions(a0, 5)
+        envs[1].sample_actions(envs[1]._act_buf, 5)
+        a1.copy_(envs[1]._act_buf)  # the same actions, int32 or (from step 16) int64
+        envs[0].step(a0)
+        envs[1].step(a1)
+        assert torch.equal(envs[0].grids(), envs[1].grids()), s
+        for name in ("accu", "counts", "pos", "rng_step", "done", "reward", "wind"):
+            assert torch.equal(getattr(envs[0], name), getattr(envs[1], name)), (name, s)
+    assert envs[1]._ctx["time"] is envs[1].accu and envs[1]._ctx["position"] is envs[1].pos
+    # step_random with its action buffer swapped for another tensor
+    b0 = torch.zeros((E, 2), dtype=torch.int32, device=device)
+    for s in range(8):
+        out1 = torch.full((E, 2), -1, dtype=torch.int32, device=device)  # a new tensor every step
+        envs[0].step_random(3, b0)
+        envs[1].step_random(3, out1)
+        assert torch.equal(b0, out1) and torch.equal(envs[0].grids(), envs[1].grids()), s
+    with pytest.raises(ValueError):
+        envs[1].accu = envs[1].accu.to(torch.float32)
+    with pytest.raises(ValueError):
+        envs[1].pos = torch.zeros((E, 3), dtype=torch.int32, device=device)
+    with pytest.raises(ValueError):
+        envs[1].step_random(3, b0.to(torch.int64))
 
 
 @pytest.mark.parametrize("N,parts", [(256, True), (512, True), (256, False)])
