@@ -163,25 +163,30 @@ def dry_run(args):
     done = (gid % 3 == 0).to(torch.uint8)
     ret = -gid.to(torch.float32) / 8
     length = gid.to(torch.int32) + 1
-    d, r, ln = (x.reshape(-1) for x in gd.all_gather_stats(done, ret, length))
+    stats = gd.StatsGather(cnt, "cpu")  # the bench's own gather (bench_alex), on gloo
+    d, r, ln = (x.reshape(-1) for x in stats.gather(done, ret, length))
     allid = torch.arange(total)
     ok = (torch.equal(d, (allid % 3 == 0).to(torch.uint8)) and torch.equal(r, -allid.to(torch.float32) / 8)
           and torch.equal(ln, allid.to(torch.int32) + 1))
+    check = gd.verify_gather(stats)  # the same self-check the real N-rank path reports
     oks = [None] * world
     if world > 1:
         dist.all_gather_object(oks, (rank, off, cnt, bool(ok)))
     else:
         oks = [(rank, off, cnt, bool(ok))]
+    all_ok = all(o for *_, o in oks) and (check is None or check["gather_ok"])
     if rank == 0:
         print(json.dumps({"metric": "dry-run", "n_gpus": world, "backend": "gloo" if world > 1 else "none",
                           "dry_run": True, "ranks": [{"rank": a, "env_offset": b, "envs": c, "gather_ok": o}
                                                      for a, b, c, o in oks],
-                          "gather_ok": all(o for *_, o in oks),
+                          "gather_ok": all_ok,
+                          "gather_check": check,
+                          "rccl_world": None if check is None else check["world_seen"],
                           "cpu_baseline": None if cpu_legs is None else cpu_legs["alex"],
                           "cpu_legs": cpu_legs}))
     if world > 1:
         dist.destroy_process_group()
-    return 0 if all(o for *_, o in oks) else 1
+    return 0 if all_ok else 1
 
 
 def synthetic_state(env, rank, device):
@@ -235,7 +240,7 @@ def timed_loop(step_fn, K, W, pg, device, reps=1, detail=None, prepare=None):
         prepare()
     for _ in range(W):
         step_fn(None)
-    events, dts = [], []
+    events, dts, per_rank = [], [], []
     for _ in range(max(1, reps)):
         if prepare is not None:
             prepare()
@@ -251,16 +256,20 @@ def timed_loop(step_fn, K, W, pg, device, reps=1, detail=None, prepare=None):
             pg.barrier()
         torch.cuda.synchronize(device)
         dt = time.perf_counter() - t0
-        if pg is not None:
-            t = torch.tensor([dt], dtype=torch.float64, device=device)
-            pg.all_reduce(t, op=pg.ReduceOp.MAX)
-            dt = float(t.item())
+        if pg is not None:  # every rank's own time (one-hot rows summed), the job's time = the max over ranks
+            t = torch.zeros(pg.get_world_size(), dtype=torch.float64, device=device)
+            t[pg.get_rank()] = dt
+            pg.all_reduce(t)
+            per_rank.append(t.tolist())
+            dt = float(t.max().item())
         dts.append(dt)
     kern = [a.elapsed_time(b) * 1e-3 for a, b in events]
     med = sorted(dts)[len(dts) // 2]
     if detail is not None:
         detail["reps_ms_per_step"] = [d / K * 1e3 for d in dts]
         detail["median_of"] = len(dts)
+        if per_rank:  # the median repetition's per-rank ms per step
+            detail["per_rank_ms_per_step"] = [x / K * 1e3 for x in per_rank[dts.index(med)]]
     return med, (sum(kern) / len(kern) if kern else None)
 
 
@@ -316,6 +325,8 @@ def bench_alex(args, world, rank, device, pg):
         "kernel": ("alex_march_kernel" if getattr(env, "march", False) else
                    "alex_step_kernel" + {"packed": "<ES, PK>", "edge": "<ES>", "planes": ""}[args.slope_layout]),
         "kernel_key": headline_kernel_key(env),
+        # N > 1: the last timed gather checked against every rank's payload over the group (None at N = 1)
+        "gather_check": gd.verify_gather(stats) if args.gather != "none" else None,
     }
     if getattr(env, "march", False) and rank == 0:
         res["tiled_kernel_ms"] = tiled_kernel_ms(env, device)
@@ -609,6 +620,7 @@ def bench_windy512(args, world, rank, device, pg):
         gather()
 
     dt_g, _ = timed_loop(seg, Kg, 0, pg, device, reps=3, prepare=restore)
+    check = gd.verify_gather(stats)
     # CA-only at HBM scale: one forced Windy step of every env, 268 MB per buffer (beyond the 256 MB
     # Infinity Cache, unlike config 2's 64 MiB pair), dense {0:.1, 3:.6, 25:.3}, beside a same-size copy
     ca = windy_ca_only(env, K, args.warmup, pg, device)
@@ -624,6 +636,7 @@ def bench_windy512(args, world, rank, device, pg):
             "gather": ("RCCL all_gather_into_tensor of reward f32 | length | done u8 per env into a reused buffer "
                        f"(gymca_amd.distributed.StatsGather: 1 pack + 1 collective), world {world}")
                       if world > 1 else "none (1 GPU)",
+            "gather_check": check,
             "ca_only_cell_updates_per_s": world * E * N * N / ca["kernel_s"],
             "ca_kernel_ms": ca["kernel_s"] * 1e3,
             "ca_achieved_gbs": WINDY_BYTES_PER_CELL * E * N * N / ca["kernel_s"] / 1e9,
@@ -1124,7 +1137,12 @@ def main():
                        "parallelism": f"env-sharded x{world}" + (
                            f", RCCL all_gather of done/return/length per step ({args.gather})"
                            if world > 1 and args.gather != "none" else "")},
-            "rccl_world": world if pg is not None else None,
+            # N > 1: the world size RCCL reported (an all_reduce of ones over the nccl group), the headline loop's last
+            # gather verified against every rank's payload, and every rank's own ms per step; null at N = 1
+            "rccl_world": None if alex["gather_check"] is None else alex["gather_check"]["world_seen"],
+            "gather_ok": None if alex["gather_check"] is None else alex["gather_check"]["gather_ok"],
+            "gather_check": alex["gather_check"],
+            "per_rank_ms_per_step": alex["timing"].get("per_rank_ms_per_step"),
             "envs_total": world * args.envs,
             "timing": dict(alex["timing"], note="value / ms_per_step = the median of the repetitions, each "
                                                 "exactly `steps` steps between barrier + synchronize"),

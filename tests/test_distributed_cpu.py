@@ -149,6 +149,8 @@ def test_bench_gpus2_dry_run_spawns_two_gloo_ranks():
     assert rc == 0, err[-2000:]
     assert out["n_gpus"] == 2 and out["backend"] == "gloo" and out["gather_ok"]
     assert [(r["rank"], r["env_offset"], r["envs"]) for r in out["ranks"]] == [(0, 0, 7), (1, 7, 7)]
+    chk = out["gather_check"]  # the real N-rank path's self-check (StatsGather.verify), here on gloo
+    assert chk["gather_ok"] and chk["rank_ok"] == [True, True] and chk["world_seen"] == 2 == out["rccl_world"]
     assert out["cpu_baseline"] is None
 
 
@@ -207,6 +209,7 @@ def test_bench_torchrun_eight_ranks_rehearsal():
     out = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
     assert out["n_gpus"] == 8 and out["gather_ok"]
     assert [(r["rank"], r["env_offset"], r["envs"]) for r in out["ranks"]] == [(k, 5 * k, 5) for k in range(8)]
+    assert out["gather_check"]["rank_ok"] == [True] * 8 and out["rccl_world"] == 8
 
 
 def test_bench_refuses_a_world_size_mismatch():
@@ -257,3 +260,48 @@ def test_all_gather_stats_does_not_keep_destroyed_groups():
     for p in ps:
         p.join(timeout=60)
     assert res == [(0, 0, 0), (1, 0, 0)], res
+
+
+def _verify_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+
+    from gymca_amd import distributed as gd
+
+    try:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        E = 6
+        g = gd.StatsGather(E, "cpu")
+        base = torch.arange(E, dtype=torch.float32) + 10 * rank
+        for step in range(3):
+            g.gather((base > 2 + step).to(torch.uint8), base + step, torch.full((E,), step, dtype=torch.int32))
+        clean = g.verify()
+        # a corrupted delivery on rank 1: one byte of rank 0's row in the buffer the last gather wrote
+        if rank == 1:
+            g.out[(g.k - 1) % len(g.out)][0, 5] ^= 0x40
+        bad = g.verify()
+        q.put((rank, clean, bad))
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        q.put((rank, repr(e), None))
+
+
+def test_stats_gather_verify_detects_a_corrupted_row():
+    """StatsGather.verify (bench.py's gather_check / rccl_world at N > 1) on gloo world 2: a clean
+    gather passes on both ranks with world_seen = 2; one flipped byte in the buffer rank 1 received fails rank 1 only,
+    and both ranks report it (gather_ok False, rank_ok [True, False])."""
+    import multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_verify_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted((q.get(timeout=120) for _ in ps), key=lambda t: t[0])
+    for p in ps:
+        p.join(timeout=60)
+    for rank, clean, bad in res:
+        assert isinstance(clean, dict), clean
+        assert clean["gather_ok"] and clean["world_seen"] == 2 and clean["rank_ok"] == [True, True]
+        assert not bad["gather_ok"] and bad["rank_ok"] == [True, False]
