@@ -330,6 +330,7 @@ def bench_alex(args, world, rank, device, pg):
     }
     if getattr(env, "march", False) and rank == 0:
         res["tiled_kernel_ms"] = tiled_kernel_ms(env, device)
+    res["pattern_floor_ms"] = march_pattern_ms(env, device)
     if args.headline_only:
         return res
     # the full reference env step: + the RGB observation of stateless_step (advanced_bulldozer.py:1120). The reference's
@@ -380,26 +381,42 @@ def bench_alex(args, world, rank, device, pg):
     action3 = torch.zeros((E, 3), dtype=torch.int32, device=device)
     action3[:, 2] = 1
 
-    def step_ext(events):
-        call("gca_random_actions", dev.ptr(action), E, env.env_offset, 7, dev.ptr(env.rng_step), st)
-        if events is not None:
-            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            a.record()
-        if fused_ext:
-            env.ca_step(render=True, action=action3)
-        else:
-            env.ca_step()
-            env.post_step(action, stats=True)
-            env.render_observation(action3)
-        if events is not None:
-            b.record()
-            events.append((a, b))
-        if fused_ext:
-            env.post_step(action, stats=True)
-            env.finish_frame(action3)
+    def make_step_ext(acts, fused_path, mixed):
+        def step_ext(events):
+            call("gca_random_actions", dev.ptr(action), E, env.env_offset, 7, dev.ptr(env.rng_step), st)
+            if mixed:  # a uniform extension choice per env and step (0 none, 1 unblur, 2 see-invisible-fires)
+                torch.remainder(action[:, 0], 3, out=acts[:, 2])
+            if events is not None:
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+            if fused_path:
+                env.ca_step(render=True, action=acts)
+                env.post_step(action, stats=True)
+                env.finish_frame(acts)
+            else:
+                env.ca_step()
+                env.post_step(action, stats=True)
+                env.render_observation(acts)
+            if events is not None:  # both paths: CA step + env step + the whole frame (refits and pixel included)
+                b.record()
+                events.append((a, b))
+        return step_ext
 
-    dt_ext, kern_ext = timed_loop(step_ext, args.steps, args.warmup, pg, device, reps=3, prepare=prep)
+    dt_ext, kern_ext = timed_loop(make_step_ext(action3, fused_ext, False), args.steps, args.warmup, pg, device, reps=3,
+                                  prepare=prep)
     refits = int(env._refit.sum().item()) if fused_ext else None
+    # a policy mixing the three extension choices (choice 0 leaves the blurred base grid to the refit pass)
+    # through the fused path and through the separate-pass path, the same steps
+    action3m = action3.clone()
+    mixed = {}
+    for name, fp in ((("fused", True),) if fused_ext else ()) + (("separate_pass", False),):
+        dtm, km = timed_loop(make_step_ext(action3m, fp, True), args.steps, args.warmup, pg, device, reps=3,
+                             prepare=prep)
+        mixed[name] = {"env_steps_per_s": world * E * args.steps / dtm, "ms_per_step": dtm / args.steps * 1e3,
+                       "step_and_frame_kernels_ms": km * 1e3}
+        if fp:
+            mixed[name]["refit_envs_last_step"] = int(env._refit.sum().item())
+    pattern_frame = march_pattern_ms(env, device, frame=True) if fused else None
     env.obs_params, env.enable_extensions = plain_params, plain_ext
     res["with_rgb_observation"] = {"env_steps_per_s": world * E * args.steps / dt_rgb,
                                    "cell_updates_per_s": world * E * N * N * args.steps / dt_rgb,
@@ -408,6 +425,9 @@ def bench_alex(args, world, rank, device, pg):
                                    "step_and_frame_kernels_ms": kern_rgb * 1e3,
                                    "observation_cost_ms": (kern_rgb - kern) * 1e3,
                                    "same_buffer_fill_ms": kern_fill * 1e3,
+                                   "pattern_floor_ms": pattern_frame,
+                                   "kernel_over_pattern_floor": (kern_rgb * 1e3 / pattern_frame
+                                                                 if pattern_frame else None),
                                    "note": "the reference's default env step (stateless_step renders RGB f32, "
                                            "enable_extensions=False): the frame from the CA step's epilogue"}
     res["with_rgb_observation_extensions"] = {
@@ -416,6 +436,7 @@ def bench_alex(args, world, rank, device, pg):
         "fused": fused_ext,
         ("step_and_frame_kernels_ms" if fused_ext else "step_and_separate_frame_ms"): kern_ext * 1e3,
         "refit_envs_last_step": refits,
+        "mixed_choice_policy": mixed,
         "note": ("enable_extensions=True, unblur chosen: the frame from the CA step's epilogue "
                  "(gca_alex_step_march_rgb_ext), refit envs by gca_adv_observation after the env step" if fused_ext else
                  "enable_extensions=True, unblur chosen: its own pass (gca_adv_observation)")}
@@ -1056,23 +1077,65 @@ def profile_entry(args, key):
 
 
 def copy_bandwidth(device, nbytes=2 << 30, reps=10):
-    """Live device-to-device copy rate (GB/s, read + write) of torch's copy kernel on this GPU, reported
-    beside the 8 TB/s spec (SURVEY.md §8d asks for both). It is a lower bound on the practical ceiling:
-    scripts/bw_probe.hip measures the alex_step access pattern itself."""
+    """Live device copy rate (GB/s, read + write) of the library's hand-written 16-B grid-stride copy (gca_bench_copy,
+    gca_bench.hip) over 2 GiB (8x the 256 MB Infinity Cache), plain and non-temporal, HIP events over `reps` launches
+    after a warm-up: the practical HBM ceiling on this device, reported beside the 8 TB/s spec (the guide's float4
+    copy: 6.29 TB/s). Returns (best GB/s, {variant: GB/s})."""
     import torch
+
+    from gymca_amd import _device as dev
+    from gymca_amd._lib import call
 
     a = torch.empty(nbytes, dtype=torch.uint8, device=device)
     b = torch.empty_like(a)
-    b.copy_(a)
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(reps):
-        b.copy_(a)
-    e.record()
-    e.synchronize()
-    gbs = 2.0 * nbytes * reps / (s.elapsed_time(e) * 1e-3) / 1e9
+    a.fill_(1)
+    st = dev.stream_ptr(device)
+    rates = {}
+    for name, nt in (("plain", 0), ("nontemporal", 1)):
+        call("gca_bench_copy", dev.ptr(a), dev.ptr(b), nbytes, nt, st)
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(reps):
+            call("gca_bench_copy", dev.ptr(a), dev.ptr(b), nbytes, nt, st)
+        e.record()
+        e.synchronize()
+        rates[name] = 2.0 * nbytes * reps / (s.elapsed_time(e) * 1e-3) / 1e9
     del a, b
-    return gbs
+    return max(rates.values()), rates
+
+
+def march_pattern_ms(env, device, frame=False, K=10, reps=3):
+    """The headline kernel's access-pattern floor in this run (gca_bench_march_pattern: gca_alex_step_march's loads and
+    stores at W = 256 with trivial arithmetic, on the env's own packed-layout buffers; frame=True adds the fused frame's
+    RGB stores at the frame kernel's 2 waves / SIMD): mean launch time from HIP events, median of `reps`. Scratch
+    outputs (the env's state is untouched; the frame buffer is rewritten by the next rendered step). None off the
+    marching step."""
+    import torch
+
+    from gymca_amd import _device as dev
+    from gymca_amd._lib import call
+
+    if not getattr(env, "march", False) or env.ncols != 256:
+        return None
+    E, H, W = env.num_envs, env.nrows, env.ncols
+    a = env.cur
+    go, ao = torch.empty_like(env.grid[a]), torch.empty_like(env.age[a])
+    st = dev.stream_ptr(device)
+    args = (int(env.alex_params.R), E, H, W, dev.ptr(env.grid[a]), dev.ptr(go), dev.ptr(env.age[a]), dev.ptr(ao),
+            dev.ptr(env.vd), dev.ptr(env.dous_bits), dev.ptr(env.slope_data), dev.ptr(env.rgb if frame else None), st)
+    times = []
+    for _ in range(reps):
+        for _ in range(3):
+            call("gca_bench_march_pattern", *args)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(K):
+            call("gca_bench_march_pattern", *args)
+        e1.record()
+        e1.synchronize()
+        times.append(e0.elapsed_time(e1) / K)
+    del go, ao
+    return sorted(times)[len(times) // 2]
 
 
 def main():
@@ -1116,7 +1179,7 @@ def main():
     prof, prof_info = profile_entry(args, alex["kernel_key"])
     traffic = None if prof is None else prof.get("bytes_per_launch")
     valu_busy = None if prof is None else prof.get("valu_busy")
-    copy_gbs = copy_bandwidth(device)
+    copy_gbs, copy_rates = copy_bandwidth(device)
     if rank == 0:
         out = {
             "metric": "cell-updates/sec, 4096x(256x256) ForestFireBulldozer (Alexandridis CA), per-GPU batch",
@@ -1173,7 +1236,13 @@ def main():
                          "traffic_gbs": traffic / (alex["kernel_ms"] * 1e-3) / 1e9 if traffic else None,
                          "traffic_frac": traffic / (alex["kernel_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS if traffic else None,
                          "device_copy_gbs": copy_gbs,
-                         "moved_frac_of_device_copy": alex["achieved_gbs"] / copy_gbs},
+                         "device_copy": dict(copy_rates, kernel="gca_bench_copy: 16-B grid-stride copy of 2 GiB, "
+                                                                "4 x 16 B in flight per thread"),
+                         "moved_frac_of_device_copy": alex["achieved_gbs"] / copy_gbs,
+                         # the same run's floor of the headline kernel's own access pattern (gca_bench_march_pattern)
+                         "pattern_floor_ms": alex.get("pattern_floor_ms"),
+                         "kernel_over_pattern_floor": (alex["kernel_ms"] / alex["pattern_floor_ms"]
+                                                       if alex.get("pattern_floor_ms") else None)},
             "cpu_baseline": cpu,
             "secondary": secondary,
             "config4": config4,

@@ -1,0 +1,165 @@
+// gca_bench.hip — measurement yardsticks the bench times in the same run as the kernels they bound:
+//
+//   gca_bench_copy            a hand-written 16-B grid-stride device copy (each thread keeps 4 x 16 B in flight,
+//                             loads before stores; plain or non-temporal), the device's practical HBM ceiling for a
+//                             buffer far beyond the 256 MB Infinity Cache (the bench uses 2 GiB)
+//   gca_bench_march_pattern   the headline kernel's exact access pattern (alex_march_kernel<R, OBS, *, 1> at W = 256:
+//                             one wave per 16-row strip of one env, lane = 4 columns, the XCD-aware block order, 3
+//                             waves / SIMD, 2 with the frame) with the rule's arithmetic replaced by a few VALU ops:
+//                             the fire ring's row R + 1 ahead, the four edge-slope planes of row r + 1 (16 B per lane,
+//                             non-temporal), vd and the dousing bits of row r, ages (8 B per lane), the grid / ages
+//                             stores, and with `rgb` the fused frame's three 1-KiB f32 stores per wave-row. It reads
+//                             and writes the same 23.125 B / cell (+ 12 written with the frame) as the step, so its
+//                             time is the floor of that pattern on this device: kernel_ms / pattern_ms says how far the
+//                             step's instruction stream sits above it.
+#include "gca_common.h"
+
+typedef float gvf4 __attribute__((ext_vector_type(4)));
+typedef uint32_t gvu2 __attribute__((ext_vector_type(2)));
+
+__global__ __launch_bounds__(256) void bench_copy_kernel(const gvf4* __restrict__ src, gvf4* __restrict__ dst,
+                                                         int64_t n4, int nt) {
+    const int64_t stride = (int64_t)gridDim.x * 256 * 4;
+    for (int64_t base = (int64_t)blockIdx.x * 256 * 4 + threadIdx.x; base < n4; base += stride) {
+        gvf4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int64_t i = base + 256 * k;
+            if (i < n4) v[k] = nt ? __builtin_nontemporal_load(src + i) : src[i];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int64_t i = base + 256 * k;
+            if (i < n4) {
+                if (nt)
+                    __builtin_nontemporal_store(v[k], dst + i);
+                else
+                    dst[i] = v[k];
+            }
+        }
+    }
+}
+
+extern "C" int gca_bench_copy(const void* src, void* dst, int64_t nbytes, int nt, void* stream) {
+    GCA_CHECK_ARG(src && dst, "src/dst required");
+    GCA_CHECK_ARG(nbytes >= 0 && nbytes % 16 == 0, "nbytes must be a multiple of 16");
+    GCA_CHECK_ARG(((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 15) == 0, "src/dst must be 16-B aligned");
+    if (nbytes == 0) return GCA_OK;
+    const int64_t n4 = nbytes / 16;
+    const int64_t want = (n4 + 1023) / 1024;
+    const unsigned blocks = (unsigned)(want < 256 * 16 ? want : 256 * 16);  // 16 workgroups per CU, grid-stride
+    hipLaunchKernelGGL(bench_copy_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const gvf4*)src,
+                       (gvf4*)dst, n4, nt ? 1 : 0);
+    GCA_CHECK_LAUNCH("bench_copy");
+    return GCA_OK;
+}
+
+template <int R, bool FRAME>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FRAME ? 2 : 3, FRAME ? 2 : 3))) void
+bench_march_pattern_kernel(int H, int nwaves, const uint8_t* __restrict__ g, uint8_t* __restrict__ go,
+                           const int16_t* __restrict__ a, int16_t* __restrict__ ao, const uint8_t* __restrict__ vd,
+                           const uint16_t* __restrict__ db, const float* __restrict__ es, gvf4* __restrict__ rgb) {
+    constexpr int W = 256, SH = 16, NF = 2 * R + 2;
+    const int lane = threadIdx.x & 63, wl = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nb = (int)gridDim.x, xcd = (int)blockIdx.x & 7, slot = (int)blockIdx.x >> 3;  // the step's XCD order
+    const int qn8 = nb >> 3, rn8 = nb & 7;
+    const int lb = (xcd < rn8 ? xcd * (qn8 + 1) : rn8 * (qn8 + 1) + (xcd - rn8) * qn8) + slot;
+    const int wv = lb * 4 + wl;
+    if (wv >= nwaves) return;
+    const int strips = H / SH, e = wv / strips, s0 = (wv - e * strips) * SH;
+    const uint32_t HW = (uint32_t)H * W;
+    const uint8_t* gE = g + (size_t)e * HW;
+    const gvf4* sE = reinterpret_cast<const gvf4*>(es + (size_t)e * 4 * HW);
+    const uint8_t* vE = vd + (size_t)e * HW;
+    const int16_t* aE = a + (size_t)e * HW;
+    const uint16_t* dE = db + (size_t)e * (HW >> 4);
+    uint32_t ring[NF];
+#pragma unroll
+    for (int k = 0; k < NF; ++k) {
+        const int r = s0 - R - 1 + k;
+        ring[k] = (r >= 0 && r < H) ? *reinterpret_cast<const uint32_t*>(gE + r * W + 4 * lane) : 0u;
+    }
+    gvf4 sl[3][4];
+    uint32_t gn[2], vv[2], dd[2];
+    gvu2 ag[2];
+    auto slopes = [&](int rs, gvf4(&o)[4]) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) o[k] = __builtin_nontemporal_load(&sE[(k * HW + (uint32_t)rs * W) / 4 + lane]);
+    };
+    auto issue = [&](int i, int sl_slot) {
+        const int r = s0 + i;
+        const int rs = min(r + 1, H - 1);
+        const uint32_t lo = (uint32_t)(r * W + 4 * lane);
+        slopes(rs, sl[(sl_slot + 1) % 3]);
+        const int rg = r + R + 1;
+        gn[sl_slot & 1] = rg < H ? *reinterpret_cast<const uint32_t*>(gE + lo + (R + 1) * W) : 0u;
+        vv[sl_slot & 1] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(vE + lo));
+        dd[sl_slot & 1] = dE[lo >> 4];
+        ag[sl_slot & 1] = __builtin_nontemporal_load(reinterpret_cast<const gvu2*>(aE + lo));
+    };
+    slopes(s0, sl[0]);
+    issue(0, 0);
+    uint32_t vsum = 0;
+#pragma unroll
+    for (int k = 0; k < NF; ++k) vsum += ring[k];
+#pragma unroll
+    for (int i = 0; i < SH; ++i) {
+        if (i + 1 < SH) issue(i + 1, i + 1);
+        const int r = s0 + i;
+        const gvf4* cur = sl[i % 3];
+        const gvf4* nxt = sl[(i + 1) % 3];
+        float acc = cur[0].x + cur[1].y + cur[2].z + cur[3].w + nxt[0].y + nxt[1].z + nxt[2].w;
+        acc += cur[0].w + cur[1].x + cur[2].y + cur[3].z + nxt[0].x + nxt[1].y + nxt[2].z;
+        const uint32_t gnew = gn[i & 1];
+        vsum += gnew - ring[i % NF];
+        ring[i % NF] = gnew;
+        const uint32_t x = vsum ^ vv[i & 1] ^ dd[i & 1];
+        const uint32_t mix = (acc > 1e30f || x == 0x12345u) ? 1u : 0u;  // never set: keeps every load live
+        const uint32_t own = ring[(i + R + 1) % NF];
+        const uint32_t lo = (uint32_t)(r * W + 4 * lane);
+        __builtin_nontemporal_store(own ^ mix, reinterpret_cast<uint32_t*>(go + (size_t)e * HW + lo));
+        gvu2 aa = ag[i & 1];
+        aa.x ^= mix;
+        __builtin_nontemporal_store(aa, reinterpret_cast<gvu2*>(ao + (size_t)e * HW + lo));
+        if constexpr (FRAME) {  // the row's f32 RGB: 3 KiB contiguous, three 1-KiB dwordx4 stores per wave
+            gvf4* fr = rgb + ((size_t)e * HW + (size_t)r * W) * 3 / 4;
+            const float m = (float)(own ^ mix);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) __builtin_nontemporal_store((gvf4){m, acc, m, (float)k}, fr + 64 * k + lane);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+template <int R>
+static void launch_pattern(int E, int H, const uint8_t* g, uint8_t* go, const int16_t* a, int16_t* ao,
+                           const uint8_t* vd, const uint16_t* db, const float* es, float* rgb, hipStream_t st) {
+    const int nwaves = E * (H / 16);
+    const dim3 grid((unsigned)((nwaves + 3) / 4));
+    if (rgb)
+        hipLaunchKernelGGL((bench_march_pattern_kernel<R, true>), grid, dim3(256), 0, st, H, nwaves, g, go, a, ao, vd, db,
+                           es, (gvf4*)rgb);
+    else
+        hipLaunchKernelGGL((bench_march_pattern_kernel<R, false>), grid, dim3(256), 0, st, H, nwaves, g, go, a, ao, vd,
+                           db, es, (gvf4*)nullptr);
+}
+
+extern "C" int gca_bench_march_pattern(int R, int E, int H, int W, const uint8_t* grid, uint8_t* grid_out,
+                                       const int16_t* age, int16_t* age_out, const uint8_t* vd,
+                                       const uint16_t* dous_bits, const float* edge_slopes, float* rgb, void* stream) {
+    GCA_CHECK_ARG(grid && grid_out && age && age_out && vd && dous_bits && edge_slopes, "buffers required");
+    GCA_CHECK_ARG(W == 256, "the pattern of the W = 256 marching step only");
+    GCA_CHECK_ARG(E >= 1 && H >= 16 && H % 16 == 0, "E >= 1, H a multiple of 16");
+    GCA_CHECK_ARG((int64_t)E * H * W < (int64_t)1 << 31, "E * H * W must stay below 2^31");
+    GCA_CHECK_ARG(((uintptr_t)edge_slopes & 15) == 0 && (!rgb || ((uintptr_t)rgb & 15) == 0), "16-B alignment");
+    hipStream_t st = (hipStream_t)stream;
+    switch (R) {
+        case 4: launch_pattern<4>(E, H, grid, grid_out, age, age_out, vd, dous_bits, edge_slopes, rgb, st); break;
+        case 5: launch_pattern<5>(E, H, grid, grid_out, age, age_out, vd, dous_bits, edge_slopes, rgb, st); break;
+        case 6: launch_pattern<6>(E, H, grid, grid_out, age, age_out, vd, dous_bits, edge_slopes, rgb, st); break;
+        case 7: launch_pattern<7>(E, H, grid, grid_out, age, age_out, vd, dous_bits, edge_slopes, rgb, st); break;
+        default: gca_set_error("argument: R must be 4..7"); return GCA_ERR_ARG;
+    }
+    GCA_CHECK_LAUNCH("bench_march_pattern");
+    return GCA_OK;
+}

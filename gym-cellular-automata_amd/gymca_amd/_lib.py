@@ -221,6 +221,8 @@ _SIGNATURES = {
     "gca_hidden_init": ([c_uint64, c_int, c_int, c_int, c_int, P, P, P, P, P, P, P, P], c_int),
     "gca_ds_count_draws": ([P, c_int, c_int, c_int, c_int, c_int, c_int, P, P], c_int),
     "gca_ds_step": ([P, P, c_int, c_int, c_int, c_int, c_int, c_int, P, P, P, c_uint64, P, c_int, P, P], c_int),
+    "gca_bench_copy": ([P, P, c_int64, c_int, P], c_int),
+    "gca_bench_march_pattern": ([c_int, c_int, c_int, c_int, P, P, P, P, P, P, P, P, P], c_int),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGNATURES)

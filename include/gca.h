@@ -467,6 +467,17 @@ int gca_ds_step(const uint8_t* grid_in, uint8_t* grid_out, int E, int H, int W, 
                 const double* uniforms, const int64_t* uniform_offset, uint64_t seed, const uint32_t* rng_step,
                 int env_offset, int32_t* counts, void* stream);
 
+/* ------------------------------------------ measurement yardsticks (bench.py; no reference counterpart)
+ * gca_bench_copy: a 16-B grid-stride device copy of nbytes (a multiple of 16, 16-B aligned), nt != 0 non-temporal
+ * loads and stores: the practical HBM ceiling the bench reports beside the 8 TB/s spec.
+ * gca_bench_march_pattern: the loads and stores of gca_alex_step_march at W = 256 (radius R in 4..7; with rgb != NULL
+ * also the fused frame's f32 RGB stores) with trivial arithmetic, on the env's packed-layout buffers: the floor of
+ * that access pattern on this device. Outputs are scratch (their values mean nothing). */
+int gca_bench_copy(const void* src, void* dst, int64_t nbytes, int nt, void* stream);
+int gca_bench_march_pattern(int R, int E, int H, int W, const uint8_t* grid, uint8_t* grid_out, const int16_t* age,
+                            int16_t* age_out, const uint8_t* vd, const uint16_t* dous_bits, const float* edge_slopes,
+                            float* rgb, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
