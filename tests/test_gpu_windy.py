@@ -264,6 +264,38 @@ def test_batched_env_graph_replay_equals_eager(device):
         assert torch.equal(torch.nan_to_num(ta), torch.nan_to_num(tb)), name
 
 
+@pytest.mark.parametrize("N,G", [(256, 32), (512, 8)])
+def test_step_random_graph_replay_equals_eager(device, N, G):
+    """The bench's capturable Windy path: a HIP graph of G env.step_random calls (one launch per
+    env step: the random policy's draw inside the fused step) leaves every env exactly as G eager step_random calls
+    do, and both equal sample_actions + step."""
+    import torch
+
+    from gymca_amd.forest_fire.bulldozer import BatchedForestFireBulldozerEnv
+    from gymca_amd.graph import StepGraph
+
+    E = 128
+    envs = [BatchedForestFireBulldozerEnv(E, N, N, device=device, seed=8, materialize_obs=False) for _ in range(3)]
+    outs = [torch.zeros((E, 2), dtype=torch.int32, device=device) for _ in range(3)]
+    for env in envs:
+        env.reset(seed=3)
+        _dense_state(env, device, seed=4, p_fire=0.05)
+    graph = StepGraph(lambda: envs[0].step_random(9, outs[0]), n_steps=G, device=device, warmup=1)
+    envs[1].step_random(9, outs[1])  # the graph's one eager warm-up step
+    envs[2].step(envs[2].sample_actions(outs[2], 9))
+    for _ in range(2):
+        graph.replay()
+        for _ in range(G):
+            envs[1].step_random(9, outs[1])
+            envs[2].step(envs[2].sample_actions(outs[2], 9))
+    torch.cuda.synchronize(device)
+    for other in envs[1:]:
+        assert torch.equal(envs[0].grids(), other.grids())
+        for name in ("pos", "accu", "rng_step", "done", "counts", "reward", "steps_elapsed"):
+            assert torch.equal(getattr(envs[0], name), getattr(other, name)), name
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+
+
 def _windy_pair(device, E, N, seed):
     from gymca_amd.forest_fire.bulldozer import BatchedForestFireBulldozerEnv
 
