@@ -31,6 +31,10 @@
 
 #include <type_traits>
 
+#ifndef GCA_MARCH_XROW
+#define GCA_MARCH_XROW 1  // the 17th slope row of a tile from the next tile's wave through LDS (r06; 0: from HBM again)
+#endif
+
 namespace {
 
 constexpr int MW = 256;  // segment width (one wave per segment of a row; W = MW * NSEG)
@@ -232,6 +236,11 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
     // HALO: [row parity][segment + 1][edge lane 0, 1, 62, 63][item]; segments 0 and NSEG + 1 are the grid's border
     __shared__ uint32_t xch[HALO ? 2 : 1][HALO ? NSEG + 2 : 1][4][HALO ? XI : 1];
     __shared__ uint32_t qfl[HALO ? NSEG : 1];
+    // XROW (NSEG = 1): the raw planes 0..2 of each wave's first row, for the wave of the tile above, whose last rows need
+    // them as row r + 2 (the "17th row": otherwise loaded from HBM a second time, 0.75 B / cell); xok: slot valid
+    constexpr bool XROW = GCA_MARCH_XROW && !HALO;
+    __shared__ float4 xrow[XROW ? 4 : 1][3][XROW ? 64 : 1];
+    __shared__ uint32_t xok[XROW ? 4 : 1];
 
     // the wave index in SGPRs: everything derived from it (env, rows, base pointers, wind) stays scalar
     const int tid = threadIdx.x, wl = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
@@ -351,6 +360,21 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
         }
     };
 
+    // XROW: every live wave of the workgroup passes exactly one workgroup barrier, after publishing its first row's
+    // planes (or, a quiet tile, that it has none): the tile above reads them after its own barrier
+    auto xrow_publish = [&](bool ok, const float4* planes) {
+        if constexpr (XROW) {
+            if (ok) {
+#pragma unroll
+                for (int k = 0; k < 3; ++k) xrow[wl][k][lane] = planes[k];
+            }
+            if (lane == 0) xok[wl] = ok ? 1u : 0u;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+        }
+    };
+
     // ---- quiet tiles: no FIRE in this tile's rows or the row on either side at the step's input -> with p_tree = 0
     //      nothing in the tile can change (a TREE burns only next to a FIRE; pinecones are a separate pass); copy it.
     //      Known from the tile activity map when the caller keeps one (gca_alex_step_packed; act_in only with
@@ -416,6 +440,7 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
             quiet = __ballot(f != 0u) == 0ull;
             if constexpr (!HALO) {
                 if (quiet) {
+                    xrow_publish(false, nullptr);
                     quiet_copy([&](int i) { return gq[i]; });
                     return;
                 }
@@ -444,6 +469,7 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
         quiet = all != 0u;
     }
     if (quiet) {  // the tile map's verdict, or every segment of a strip quiet (HALO): rows loaded again
+        xrow_publish(false, nullptr);
         quiet_copy([&](int i) { return *reinterpret_cast<const uint32_t*>(gE + (uint32_t)(s0 + i) * W + lc); });
         return;
     }
@@ -480,6 +506,9 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    xrow_publish(true, sc);  // (raw planes: prep_own below rewrites sc)
+    // the tile below is the next wave of this workgroup, in the same env, and published its first row
+    const bool xuse = XROW && wl < 3 && s0 + SH < H && xok[XROW ? wl + 1 : 0] != 0u;
     uint32_t V[R + 1];
 #pragma unroll
     for (int k = 1; k <= R; ++k) {
@@ -600,6 +629,14 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
         // last rows re-fetched it from HBM, ~1 B/cell.)
         bool need_next = i + 1 < SH;
         auto load_next_slopes = [&]() {  // row r+2's raw planes into SC
+            if constexpr (XROW) {
+                if (i == SH - 2 && xuse) {  // row r+2 = the next tile's first row: from its wave's LDS slot
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) SC[k] = xrow[wl + 1][k][lane];
+                    SC[3] = SC[2];  // plane 3 of row r+2 serves row r+2 only (the next tile's): unused here
+                    return;
+                }
+            }
             // plane 3 of row r+2 serves row r+2 itself only: the next tile's first row (i = SH - 2) skips it too.
             // A skipped load reads row 0 of env 0's planes instead (the same 4 KiB for every wave: L2-resident,
             // while the streamed planes are loaded non-temporally and do not stay)

@@ -10,10 +10,10 @@ O=$R/gym-cellular-automata_amd/gymca_amd/_lib/variants
 B=$C/build/variant_$NAME
 mkdir -p $O $B
 F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -Wno-unused-function -munsafe-fp-atomics $*"
-for s in gca_util gca_windy gca_env gca_alex gca_alex_march gca_ds gca_obs gca_pine gca_init; do
+for s in gca_util gca_windy gca_env gca_alex gca_alex_march gca_ds gca_obs gca_pine gca_init gca_bench; do
   /opt/rocm/bin/hipcc $F -c $C/$s.hip -o $B/$s.o &
 done
 wait
-for s in gca_util gca_windy gca_env gca_alex gca_alex_march gca_ds gca_obs gca_pine gca_init; do [ -f $B/$s.o ] || { echo "compile of $s failed" >&2; exit 1; }; done
+for s in gca_util gca_windy gca_env gca_alex gca_alex_march gca_ds gca_obs gca_pine gca_init gca_bench; do [ -f $B/$s.o ] || { echo "compile of $s failed" >&2; exit 1; }; done
 /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 $B/*.o -o $O/$NAME.so
 echo $O/$NAME.so
