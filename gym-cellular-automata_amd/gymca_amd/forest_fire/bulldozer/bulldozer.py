@@ -194,10 +194,13 @@ class ForestFireBulldozerEnv(CAEnv):
         if self._counts is None:
             io = self.move_modify._io
             g = self.grid
-            if io is not None and dev.is_device_tensor(g) and g.device == io.device and g.is_contiguous():
+            if (io is not None and getattr(self, "one_readback", True) and dev.is_device_tensor(g) and g.device == io.device
+                    and g.is_contiguous()):
                 self._counts = self._count_with(io, g)
             else:
                 self._counts = self.count_cells(self.grid)
+                if io is not None and io.pending is not None:  # resolve Move / Modify's hit and position now: _report
+                    io.sync_read()                              # reads them before step() ends
         return self._counts
 
     def _count_with(self, io, g):
