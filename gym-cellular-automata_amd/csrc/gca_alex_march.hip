@@ -236,9 +236,12 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
     // HALO: [row parity][segment + 1][edge lane 0, 1, 62, 63][item]; segments 0 and NSEG + 1 are the grid's border
     __shared__ uint32_t xch[HALO ? 2 : 1][HALO ? NSEG + 2 : 1][4][HALO ? XI : 1];
     __shared__ uint32_t qfl[HALO ? NSEG : 1];
-    // XROW (NSEG = 1): the raw planes 0..2 of each wave's first row, for the wave of the tile above, whose last rows need
-    // them as row r + 2 (the "17th row": otherwise loaded from HBM a second time, 0.75 B / cell); xok: slot valid
-    constexpr bool XROW = GCA_MARCH_XROW && !HALO;
+    // XROW (NSEG = 1, the fused-frame kernel): the raw planes 0..2 of each wave's first row, for the wave of the tile
+    // above, whose last rows need them as row r + 2 (the "17th row": otherwise loaded from HBM a second time, 0.75 B /
+    // cell; 3 of a workgroup's 4 tile boundaries); xok: slot valid. r06 A/B (profiles/r06a, r06b): HBM traffic 24.70 ->
+    // 24.15 B / cell; the fused-frame step -1.2 %, but the plain step +0-1.2 % (the one workgroup barrier aligns the
+    // four waves' starts) and the reset state's quiet tiles +46 % (0.345 -> 0.503 ms): the plain kernel keeps the 17th row
+    constexpr bool XROW = GCA_MARCH_XROW && !HALO && OBS;
     __shared__ float4 xrow[XROW ? 4 : 1][3][XROW ? 64 : 1];
     __shared__ uint32_t xok[XROW ? 4 : 1];
 
