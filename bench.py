@@ -1104,7 +1104,7 @@ def profile_entry(args, key):
 
 
 def copy_bandwidth(device, nbytes=2 << 30, reps=10):
-    """Live device copy rate (GB/s, read + write) of the library's hand-written 16-B grid-stride copy (gca_bench_copy,
+    """Live device copy rate (GB/s, read + write) of the library's hand-written 16-B copy (gca_bench_copy,
     gca_bench.hip) over 2 GiB (8x the 256 MB Infinity Cache), plain and non-temporal, HIP events over `reps` launches
     after a warm-up: the practical HBM ceiling on this device, reported beside the 8 TB/s spec (the guide's float4
     copy: 6.29 TB/s). Returns (best GB/s, {variant: GB/s})."""
@@ -1263,8 +1263,8 @@ def main():
                          "traffic_gbs": traffic / (alex["kernel_ms"] * 1e-3) / 1e9 if traffic else None,
                          "traffic_frac": traffic / (alex["kernel_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS if traffic else None,
                          "device_copy_gbs": copy_gbs,
-                         "device_copy": dict(copy_rates, kernel="gca_bench_copy: 16-B grid-stride copy of 2 GiB, "
-                                                                "4 x 16 B in flight per thread"),
+                         "device_copy": dict(copy_rates, kernel="gca_bench_copy: 16-B copy of 2 GiB, one element "
+                                                                "per thread, one pass"),
                          "moved_frac_of_device_copy": alex["achieved_gbs"] / copy_gbs,
                          # the same run's floor of the headline kernel's own access pattern (gca_bench_march_pattern)
                          "pattern_floor_ms": alex.get("pattern_floor_ms"),

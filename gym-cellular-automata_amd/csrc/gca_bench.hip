@@ -1,8 +1,8 @@
 // gca_bench.hip — measurement yardsticks the bench times in the same run as the kernels they bound:
 //
-//   gca_bench_copy            a hand-written 16-B grid-stride device copy (each thread keeps 4 x 16 B in flight,
-//                             loads before stores; plain or non-temporal), the device's practical HBM ceiling for a
-//                             buffer far beyond the 256 MB Infinity Cache (the bench uses 2 GiB)
+//   gca_bench_copy            a hand-written 16-B device copy (one element per thread, one pass; plain or
+//                             non-temporal), the device's practical HBM ceiling for a buffer far beyond the 256 MB
+//                             Infinity Cache (the bench uses 2 GiB)
 //   gca_bench_march_pattern   the headline kernel's exact access pattern (alex_march_kernel<R, OBS, *, 1> at W = 256:
 //                             one wave per 16-row strip of one env, lane = 4 columns, the XCD-aware block order, 3
 //                             waves / SIMD, 2 with the frame) with the rule's arithmetic replaced by a few VALU ops:
@@ -17,39 +17,28 @@
 typedef float gvf4 __attribute__((ext_vector_type(4)));
 typedef uint32_t gvu2 __attribute__((ext_vector_type(2)));
 
+// one 16-B element per thread, one pass (no grid-stride loop): the fastest of 21 forms on this pool's boxes, 6.25-6.28
+// TB/s at 1 / 2 / 4 GiB against 5.0-5.7 for grid-stride loops with 1-8 elements in flight (scripts/copy_probe.hip,
+// profiles/r06d/copy.json) -- the guide's 6.29 TB/s float4 copy
 __global__ __launch_bounds__(256) void bench_copy_kernel(const gvf4* __restrict__ src, gvf4* __restrict__ dst,
                                                          int64_t n4, int nt) {
-    const int64_t stride = (int64_t)gridDim.x * 256 * 4;
-    for (int64_t base = (int64_t)blockIdx.x * 256 * 4 + threadIdx.x; base < n4; base += stride) {
-        gvf4 v[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int64_t i = base + 256 * k;
-            if (i < n4) v[k] = nt ? __builtin_nontemporal_load(src + i) : src[i];
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int64_t i = base + 256 * k;
-            if (i < n4) {
-                if (nt)
-                    __builtin_nontemporal_store(v[k], dst + i);
-                else
-                    dst[i] = v[k];
-            }
-        }
-    }
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n4) return;
+    if (nt)
+        __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+    else
+        dst[i] = src[i];
 }
 
 extern "C" int gca_bench_copy(const void* src, void* dst, int64_t nbytes, int nt, void* stream) {
     GCA_CHECK_ARG(src && dst, "src/dst required");
     GCA_CHECK_ARG(nbytes >= 0 && nbytes % 16 == 0, "nbytes must be a multiple of 16");
     GCA_CHECK_ARG(((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 15) == 0, "src/dst must be 16-B aligned");
+    GCA_CHECK_ARG(nbytes / 16 / 256 < ((int64_t)1 << 31), "nbytes too large for one pass");
     if (nbytes == 0) return GCA_OK;
     const int64_t n4 = nbytes / 16;
-    const int64_t want = (n4 + 1023) / 1024;
-    const unsigned blocks = (unsigned)(want < 256 * 16 ? want : 256 * 16);  // 16 workgroups per CU, grid-stride
-    hipLaunchKernelGGL(bench_copy_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const gvf4*)src,
-                       (gvf4*)dst, n4, nt ? 1 : 0);
+    hipLaunchKernelGGL(bench_copy_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       (const gvf4*)src, (gvf4*)dst, n4, nt ? 1 : 0);
     GCA_CHECK_LAUNCH("bench_copy");
     return GCA_OK;
 }
