@@ -743,6 +743,150 @@ __global__ __launch_bounds__(256) void bulldozer_step_fused_parts_kernel(
     if (steps_elapsed) steps_elapsed[e] = se + 1;
 }
 
+// K env steps of every env in ONE launch under the random policy of gca_bulldozer_step_fused_random (r06): one
+// workgroup per env marches its env through the K steps with the per-env state in registers (read once, written once):
+// the action drawn from (env, rng_step) exactly as gca_random_actions does, RepeatCA's time, the Windy CA over the env's
+// strips when the step takes one (every wave, one workgroup barrier before the counts), Move / Modify (thread 0) and
+// reward / done, broadcast to the workgroup through LDS behind one barrier per step. Bit for bit K calls of
+// gca_bulldozer_step_fused_random (tests/test_gpu_windy.py). Workgroups never wait for each other, so an env whose fire
+// burns out or whose CA steps are few runs ahead: the K x E env steps cost the slowest env's chain, not K launches of
+// the slowest step. Per-step outputs (optional): the actions (K, E, 2), rewards (K, E) and done flags (K, E).
+template <int NW, bool STD>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) void bulldozer_rollout_random_kernel(
+    gca_bulldozer_params p, int K, uint64_t seed, int32_t* __restrict__ action_out, double* __restrict__ reward_out,
+    uint8_t* __restrict__ done_out, double* __restrict__ accu, int32_t* __restrict__ steps, uint8_t* __restrict__ done,
+    const double* __restrict__ wind, int64_t wind_stride, uint32_t* __restrict__ rng_step, uint8_t* __restrict__ parity,
+    uint8_t* __restrict__ buf0, uint8_t* __restrict__ buf1, int H, int32_t* __restrict__ pos,
+    int32_t* __restrict__ counts, uint8_t* __restrict__ hit, double* __restrict__ reward,
+    int64_t* __restrict__ steps_elapsed, int E) {
+    constexpr int W = 256 * NW;
+    __shared__ int32_t wave_cnt[16][3];
+    __shared__ int32_t bc[2][4];  // thread 0 -> the workgroup, per step (double-buffered): E, T, F counts, hit
+    const int e = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, nw = (int)(blockDim.x >> 6);
+    const uint32_t env_id = (uint32_t)(p.env_offset + e);
+    bool was_done = done[e] != 0;
+    uint32_t rs = rng_step[e];
+    double acc = accu[e];
+    bool odd = parity[e] != 0;
+    int32_t row = pos[2 * e], col = pos[2 * e + 1];
+    int32_t cE = counts[3 * e + 0], cT = counts[3 * e + 1], cF = counts[3 * e + 2];
+    int64_t se = steps_elapsed ? steps_elapsed[e] : 0;
+    uint8_t h = hit[e];
+    double rew = reward[e];
+    int last_n = 0;
+    double wl[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) wl[k] = wind[(int64_t)e * wind_stride + k];
+    const int64_t HW = (int64_t)H * W;
+    const uint32_t lofs = 4 * NW * (uint32_t)lane;
+    for (int k = 0; k < K; ++k) {
+        int32_t act0, act1;
+        fused_action(nullptr, FusedPolicy{seed, nullptr}, e, env_id, rs, act0, act1);
+        const size_t ke = (size_t)k * E + e;
+        if (action_out && tid == 0) {
+            action_out[2 * ke] = act0;
+            action_out[2 * ke + 1] = act1;
+        }
+        const int a0 = clampi_dev(act0, 0, 8), a1s = clampi_dev(act1, 0, 1);
+        const double x = acc + ((p.t_move[a0] + p.t_shoot[a1s]) + p.t_any);
+        const double reps = trunc(x);
+        const int n = was_done ? -1 : (int)reps;
+        last_n = n;
+        if (n < 0) {  // finished: a graceful no-op step (ca_env.py:50-62), nothing but the reward changes
+            rew = 0.0;
+            if (tid == 0) {
+                if (reward_out) reward_out[ke] = 0.0;
+                if (done_out) done_out[ke] = 1;
+            }
+            continue;
+        }
+        int nrow = row, ncol = col;
+        move_pos(a0, nrow, ncol, H, W, p.up_mask, p.down_mask, p.left_mask, p.right_mask);
+        uint8_t* grid = (odd ? buf1 : buf0) + e * HW;
+        if (n > 0) {
+            auto get_mask = [&]() -> uint32_t { return wave_windy_mask(p, wl, e, rs, lane); };
+            const uint8_t* __restrict__ S = grid;
+            uint8_t* __restrict__ Dst = (odd ? buf0 : buf1) + e * HW;
+            int32_t cntT = 0, cntF = 0, cntV = 0;
+            for (int s0 = wave * FUSED_SH<NW>; s0 < H; s0 += nw * FUSED_SH<NW>)
+                windy_rows_strip_f<NW, FUSED_SH<NW>, FUSED_RD<NW>, STD>(S, Dst, s0, H, get_mask, lofs, rep4(p.empty),
+                                                                       rep4(p.tree), rep4(p.fire), cntT, cntF, cntV);
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) {
+                cntT += __shfl_xor(cntT, off);
+                cntF += __shfl_xor(cntF, off);
+                cntV += __shfl_xor(cntV, off);
+            }
+            if (lane == 0) {
+                wave_cnt[wave][0] = cntV - cntT - cntF;
+                wave_cnt[wave][1] = cntT;
+                wave_cnt[wave][2] = cntF;
+            }
+            __syncthreads();  // the new grid (every wave's stores) and the counts are complete
+            grid = Dst;
+            odd = !odd;
+            cE = cT = cF = 0;
+            for (int w = 0; w < nw; ++w) {
+                cE += wave_cnt[w][0];
+                cT += wave_cnt[w][1];
+                cF += wave_cnt[w][2];
+            }
+        }
+        acc = x - reps;
+        row = nrow;
+        col = ncol;
+        int32_t* B = bc[k & 1];
+        if (tid == 0) {  // MoveModify (move_modify.py:128-134): Modify at the new position, on the post-CA grid
+            uint8_t hh = 0;
+            if (act1 && row >= 0 && row < H && col >= 0 && col < W) {
+                const int v = grid[(int64_t)row * W + col];
+                const int nv = p.effect[v];
+                if (nv >= 0) {
+                    grid[(int64_t)row * W + col] = (uint8_t)nv;
+                    hh = 1;
+                    const int c_old = cell_category(v, p.empty, p.tree, p.fire);
+                    const int c_new = cell_category(nv, p.empty, p.tree, p.fire);
+                    if (c_old == 0) cE -= 1; else if (c_old == 1) cT -= 1; else if (c_old == 2) cF -= 1;
+                    if (c_new == 0) cE += 1; else if (c_new == 1) cT += 1; else if (c_new == 2) cF += 1;
+                }
+            }
+            B[0] = cE;
+            B[1] = cT;
+            B[2] = cF;
+            B[3] = hh;
+        }
+        __syncthreads();  // the Modify write and its counts, for every wave's next step
+        cE = B[0];
+        cT = B[1];
+        cF = B[2];
+        h = (uint8_t)B[3];
+        rew = (cT + cF) > 0 ? -((double)cF / (double)(cT + cF)) : (double)NAN;
+        was_done = cF == 0;
+        rs += (uint32_t)n;
+        se += 1;
+        if (tid == 0) {
+            if (reward_out) reward_out[ke] = rew;
+            if (done_out) done_out[ke] = was_done ? 1 : 0;
+        }
+    }
+    if (tid != 0 || K == 0) return;
+    steps[e] = last_n;
+    reward[e] = rew;
+    accu[e] = acc;
+    parity[e] = odd ? 1 : 0;
+    pos[2 * e] = row;
+    pos[2 * e + 1] = col;
+    counts[3 * e + 0] = cE;
+    counts[3 * e + 1] = cT;
+    counts[3 * e + 2] = cF;
+    hit[e] = h;
+    done[e] = was_done ? 1 : 0;
+    rng_step[e] = rs;
+    if (steps_elapsed) steps_elapsed[e] = se;
+}
+
 template <int NW>
 static void launch_rows(uint8_t* b0, uint8_t* b1, const uint8_t* parity, const int32_t* steps, int pass,
                         const uint8_t* dm, int E, int H, int empty, int tree, int fire, int32_t* counts,
@@ -901,4 +1045,43 @@ extern "C" int gca_bulldozer_step_fused_random(const gca_bulldozer_params* p, ui
     return bulldozer_step_fused_impl(p, nullptr, FusedPolicy{action_seed, action_out}, accu, steps, done, wind,
                                      wind_stride, rng_step, parity, buf0, buf1, H, W, pos, counts, hit, reward,
                                      steps_elapsed, meet, E, stream);
+}
+
+extern "C" int gca_bulldozer_rollout_random(const gca_bulldozer_params* p, uint64_t action_seed, int K,
+                                            int32_t* action_out, double* reward_out, uint8_t* done_out, double* accu,
+                                            int32_t* steps, uint8_t* done, const double* wind, int64_t wind_stride,
+                                            uint32_t* rng_step, uint8_t* parity, uint8_t* buf0, uint8_t* buf1, int H,
+                                            int W, int32_t* pos, int32_t* counts, uint8_t* hit, double* reward,
+                                            int64_t* steps_elapsed, int E, void* stream) {
+    GCA_CHECK_ARG(p && accu && steps && done && wind && rng_step && parity && buf0 && buf1 && pos && counts && hit &&
+                      reward && E > 0 && H > 0 && K >= 0,
+                  "bulldozer_rollout_random: null argument, empty batch or K < 0");
+    GCA_CHECK_ARG(W == 256 || W == 512, "bulldozer_rollout_random: W must be 256 or 512 (the row-stream CA)");
+    GCA_CHECK_ARG(p->empty == 0 && p->empty < p->tree && p->tree < p->fire && p->fire < 256,
+                  "bulldozer_rollout_random: cell codes must be empty = 0 < tree < fire < 256 (the closed-form rule)");
+    GCA_CHECK_ARG(((((uintptr_t)buf0) | ((uintptr_t)buf1)) & 15u) == 0, "bulldozer_rollout_random: buffers 16-B aligned");
+    GCA_CHECK_ARG(wind_stride >= 0, "bulldozer_rollout_random: wind_stride >= 0");
+    GCA_CHECK_ARG((int64_t)K * E < ((int64_t)1 << 40), "bulldozer_rollout_random: K x E too large");
+    double tmax = 0.0;
+    for (int a = 0; a < 9; ++a)
+        for (int b = 0; b < 2; ++b) tmax = fmax(tmax, (p->t_move[a] + p->t_shoot[b]) + p->t_any);
+    GCA_CHECK_ARG(tmax < 1.0, "bulldozer_rollout_random: an action can take >= 1 time unit (several CA passes per step)");
+    if (K == 0) return GCA_OK;
+    const int fsh = W == 256 ? FUSED_SH<1> : FUSED_SH<2>;
+    const int strips = (H + fsh - 1) / fsh;
+    const int threads = 64 * (strips < 16 ? strips : 16);
+    hipStream_t st = (hipStream_t)stream;
+    const bool std_codes = p->empty == 0 && p->tree == 3 && p->fire == 25;
+#define GCA_ROLLOUT_LAUNCH(NWV, STDV)                                                                                    \
+    hipLaunchKernelGGL((bulldozer_rollout_random_kernel<NWV, STDV>), dim3((unsigned)E), dim3(threads), 0, st, *p, K,    \
+                       action_seed, action_out, reward_out, done_out, accu, steps, done, wind, wind_stride, rng_step,     \
+                       parity, buf0, buf1, H, pos, counts, hit, reward, steps_elapsed, E)
+    if (W == 256) {
+        if (std_codes) GCA_ROLLOUT_LAUNCH(1, true); else GCA_ROLLOUT_LAUNCH(1, false);
+    } else {
+        if (std_codes) GCA_ROLLOUT_LAUNCH(2, true); else GCA_ROLLOUT_LAUNCH(2, false);
+    }
+#undef GCA_ROLLOUT_LAUNCH
+    GCA_CHECK_LAUNCH("bulldozer_rollout_random");
+    return GCA_OK;
 }

@@ -185,6 +185,8 @@ _SIGNATURES = {
                                   P, P, P, c_int, P], c_int),
     "gca_bulldozer_step_fused_random": ([POINTER(BulldozerParams), c_uint64, P, P, P, P, P, c_int64, P, P, P, P, c_int,
                                          c_int, P, P, P, P, P, P, c_int, P], c_int),
+    "gca_bulldozer_rollout_random": ([POINTER(BulldozerParams), c_uint64, c_int, P, P, P, P, P, P, P, c_int64, P, P, P,
+                                      P, c_int, c_int, P, P, P, P, P, c_int, P], c_int),
     "gca_move_modify": ([POINTER(BulldozerParams), P, P, P, c_int, c_int, P, c_int, P], c_int),
     "gca_alex_prepare_slope": ([P, P, c_int, c_int, c_int, P], c_int),
     "gca_alex_step": ([POINTER(AlexParams), c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P],

@@ -244,6 +244,32 @@ class BatchedForestFireBulldozerEnv:
         self._random_call[2](dev.raw_stream(self._dev_index))
         return self._obs(), self.reward, self._done_bool, self._truncated, self._info
 
+    def rollout_random(self, K, seed=9, action_out=None, reward_out=None, done_out=None):
+        """K env steps of every env in ONE launch under the random policy of step_random (gca_bulldozer_rollout_random):
+        bit for bit K calls of step_random(seed), the env's state kept in registers across the steps. Optional per-step
+        records, device tensors: action_out int32 (K, E, 2), reward_out float64 (K, E), done_out uint8 (K, E). Returns
+        (reward_out, done_out). Fused step only (W = 256 / 512, one CA pass at most per env step)."""
+        import torch
+
+        if not self.fused:
+            raise ValueError("rollout_random needs the fused step (W in (256, 512), at most one CA pass per env step)")
+        K, E = int(K), self.num_envs
+        if K < 0:
+            raise ValueError("rollout_random: K >= 0")
+        for name, t, dt, shape in (("action_out", action_out, torch.int32, (K, E, 2)),
+                                   ("reward_out", reward_out, torch.float64, (K, E)),
+                                   ("done_out", done_out, torch.uint8, (K, E))):
+            if t is not None and not (type(t) is torch.Tensor and t.dtype == dt and tuple(t.shape) == shape
+                                      and t.device == self.device and t.is_contiguous()):
+                raise ValueError(f"rollout_random: {name} must be a contiguous {dt} {shape} tensor on the env's device")
+        H, W = self.nrows, self.ncols
+        call("gca_bulldozer_rollout_random", self.params, int(seed) & (2**64 - 1), K, dev.ptr(action_out),
+             dev.ptr(reward_out), dev.ptr(done_out), dev.ptr(self.accu), dev.ptr(self.steps), dev.ptr(self.done),
+             dev.ptr(self.wind), 9, dev.ptr(self.rng_step), dev.ptr(self.parity), dev.ptr(self.buf[0]),
+             dev.ptr(self.buf[1]), H, W, dev.ptr(self.pos), dev.ptr(self.counts), dev.ptr(self.hit), dev.ptr(self.reward),
+             dev.ptr(self.steps_elapsed), E, dev.stream_ptr(self.device))
+        return reward_out, done_out
+
     def sample_actions(self, out=None, tag=9):
         """Uniform random actions for every env on the device -- the batched `action_space.sample()` (move in [0, 9),
         shoot in {0, 1}; Philox keyed by (tag, global env id, the env's rng_step)) -- into `out` (a contiguous int32

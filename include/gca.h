@@ -140,6 +140,17 @@ int gca_bulldozer_step_fused_random(const gca_bulldozer_params* p, uint64_t acti
                                     int64_t wind_stride, uint32_t* rng_step, uint8_t* parity, uint8_t* buf0,
                                     uint8_t* buf1, int H, int W, int32_t* pos, int32_t* counts, uint8_t* hit,
                                     double* reward, int64_t* steps_elapsed, uint64_t* meet, int E, void* stream);
+/* K env steps of every env in ONE launch under gca_bulldozer_step_fused_random's random policy (r06): bit for bit K
+ * consecutive gca_bulldozer_step_fused_random calls with the same action_seed (the batched form of K iterations of the
+ * reference loop `env.step(env.action_space.sample())`, bulldozer.py:393-400, ca_env.py:27-62); one workgroup per env
+ * keeps the env's state in registers across the K steps. Optional per-step outputs: action_out (K, E, 2) int32,
+ * reward_out (K, E) f64, done_out (K, E) u8 (as `done` after each step). Same contract as gca_bulldozer_step_fused
+ * (W = 256 / 512, one CA pass at most per env step, empty = 0 < tree < fire). */
+int gca_bulldozer_rollout_random(const gca_bulldozer_params* p, uint64_t action_seed, int K, int32_t* action_out,
+                                 double* reward_out, uint8_t* done_out, double* accu, int32_t* steps, uint8_t* done,
+                                 const double* wind, int64_t wind_stride, uint32_t* rng_step, uint8_t* parity,
+                                 uint8_t* buf0, uint8_t* buf1, int H, int W, int32_t* pos, int32_t* counts, uint8_t* hit,
+                                 double* reward, int64_t* steps_elapsed, int E, void* stream);
 
 /* Move then Modify for E envs (move_modify.py:37-134): action[e] = (move, shoot);
  * uses p->up/down/left/right_mask and p->effect; grid may be NULL (Move only); hit nullable. */
@@ -468,7 +479,7 @@ int gca_ds_step(const uint8_t* grid_in, uint8_t* grid_out, int E, int H, int W, 
                 int env_offset, int32_t* counts, void* stream);
 
 /* ------------------------------------------ measurement yardsticks (bench.py; no reference counterpart)
- * gca_bench_copy: a 16-B grid-stride device copy of nbytes (a multiple of 16, 16-B aligned), nt != 0 non-temporal
+ * gca_bench_copy: a 16-B device copy of nbytes (one element per thread, one pass) (a multiple of 16, 16-B aligned), nt != 0 non-temporal
  * loads and stores: the practical HBM ceiling the bench reports beside the 8 TB/s spec.
  * gca_bench_march_pattern: the loads and stores of gca_alex_step_march at W = 256 (radius R in 4..7; with rgb != NULL
  * also the fused frame's f32 RGB stores) with trivial arithmetic, on the env's packed-layout buffers: the floor of

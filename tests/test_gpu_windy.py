@@ -296,6 +296,59 @@ def test_step_random_graph_replay_equals_eager(device, N, G):
     assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
 
 
+@pytest.mark.parametrize("N,K", [(256, 40), (512, 24), (256, 1)])
+def test_rollout_random_equals_step_random(device, N, K):
+    """gca_bulldozer_rollout_random (env.rollout_random): K env steps in one launch equal K env.step_random calls bit
+    for bit -- every state tensor after the rollout, and the per-step actions, rewards and done flags against each
+    step's own -- from a state where some envs burn out during the rollout and some are finished before it."""
+    import torch
+
+    from gymca_amd import _device as dev
+    from gymca_amd._lib import call
+    from gymca_amd.forest_fire.bulldozer import BatchedForestFireBulldozerEnv
+
+    E = 192
+    envs = [BatchedForestFireBulldozerEnv(E, N, N, device=device, seed=31, env_offset=3, materialize_obs=False)
+            for _ in range(2)]
+    for env in envs:
+        env.reset(seed=7)
+        _dense_state(env, device, seed=5, p_fire=0.05)
+        g = env.grids()
+        g[:16] = torch.where(g[:16] == 25, torch.tensor(3, dtype=torch.uint8, device=device), g[:16])
+        g[:16, N // 2, N // 2] = 25  # one fire: these burn out within a few CA steps
+        env.buf[0].copy_(g)
+        env.buf[1].copy_(g)
+        env.parity.zero_()
+        call("gca_count_cells", dev.ptr(env.buf[0]), E, N, N, 0, 3, 25, dev.ptr(env.counts), dev.stream_ptr(device))
+        env.done[:4] = 1  # finished before the rollout
+        gen = torch.Generator(device=device).manual_seed(11)
+        env.accu.copy_(torch.rand(E, dtype=torch.float64, device=device, generator=gen) * 0.9)
+    a_step = torch.zeros((E, 2), dtype=torch.int32, device=device)
+    acts, rews, dones = [], [], []
+    for _ in range(K):
+        envs[0].step_random(9, a_step)
+        acts.append(a_step.clone())
+        rews.append(envs[0].reward.clone())
+        dones.append(envs[0].done.clone())
+    a_out = torch.full((K, E, 2), -1, dtype=torch.int32, device=device)
+    r_out = torch.zeros((K, E), dtype=torch.float64, device=device)
+    d_out = torch.full((K, E), 7, dtype=torch.uint8, device=device)
+    envs[1].rollout_random(K, 9, a_out, r_out, d_out)
+    torch.cuda.synchronize(device)
+    assert torch.equal(envs[0].grids(), envs[1].grids())
+    for name in ("pos", "accu", "rng_step", "done", "counts", "hit", "steps", "parity", "steps_elapsed"):
+        assert torch.equal(getattr(envs[0], name), getattr(envs[1], name)), name
+    assert torch.equal(torch.nan_to_num(envs[0].reward), torch.nan_to_num(envs[1].reward))
+    assert torch.equal(a_out, torch.stack(acts))
+    assert torch.equal(torch.nan_to_num(r_out), torch.nan_to_num(torch.stack(rews)))
+    assert torch.equal(d_out, torch.stack(dones))
+    if K > 1:
+        assert int(envs[1].steps_elapsed.sum()) > 0 and int(envs[1].done[4:16].sum()) > 0  # burn-outs happened
+    before = [t.clone() for t in (envs[1].accu, envs[1].rng_step)]
+    envs[1].rollout_random(0, 9)  # K = 0: nothing changes
+    assert torch.equal(before[0], envs[1].accu) and torch.equal(before[1], envs[1].rng_step)
+
+
 def _windy_pair(device, E, N, seed):
     from gymca_amd.forest_fire.bulldozer import BatchedForestFireBulldozerEnv
 
