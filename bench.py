@@ -542,6 +542,9 @@ def bench_windy(args, world, rank, device, pg):
         graphs[name] = world * E * reps_g * g_steps / dtg
         del graph
     best_graph = max(graphs, key=graphs.get)
+    # the same random policy, 32 env steps per launch (gca_bulldozer_rollout_random: the env's state in registers across
+    # the steps), the per-step rewards and done flags recorded
+    rollout = rollout_rate(env, 9, max(Kg * G // 32, 2) * 32, restore, pg, device, world)
     # CA-only (steps[E] = 1 forced), dense variant {0:.1, 3:.6, 25:.3}
     g = env.grids()
     u = torch.rand(g.shape, device=device)
@@ -585,6 +588,7 @@ def bench_windy(args, world, rank, device, pg):
         "env_steps_per_s_eager": world * E * Kg * G / dt_eager,
         "env_steps_per_s_random_policy_fused": world * E * Kg * G / dt_rand,
         "env_steps_per_s_graphs": graphs,
+        "env_steps_per_s_rollout_random_k32": rollout,
         "loops": f"eager, random-policy-fused and the graphs: the same {Kg * G} env steps (graphs: whole graphs, at "
                  f"least 2) from one mid-episode state (reset + 64 steps, restored before each repetition), median of 3",
         "env_step_graph": "hipGraph of env steps: sample_step_g8 = 8 x (gca_random_actions + gca_bulldozer_step_fused), "
@@ -663,6 +667,7 @@ def bench_windy512(args, world, rank, device, pg):
         graphs[name] = world * E * reps_g * g_steps / dtg
         del graph
     best_graph = max(graphs, key=graphs.get)
+    rollout = rollout_rate(env, 11, max(K // 32, 2) * 32, restore, pg, device, world, gather=gather)
     check = gd.verify_gather(stats)
     # CA-only at HBM scale: one forced Windy step of every env, 268 MB per buffer (beyond the 256 MB
     # Infinity Cache, unlike config 2's 64 MiB pair), dense {0:.1, 3:.6, 25:.3}, beside a same-size copy
@@ -688,6 +693,26 @@ def bench_windy512(args, world, rank, device, pg):
             "ca_roofline_frac": WINDY_BYTES_PER_CELL * E * N * N / ca["kernel_s"] / 1e9 / HBM_PEAK_GBS,
             "same_size_copy_ms": ca["copy_s"] * 1e3,
             "ca_frac_of_same_size_copy": ca["copy_s"] / ca["kernel_s"]}
+
+
+def rollout_rate(env, seed, steps, restore, pg, device, world, k=32, gather=None):
+    """env-steps/s of the random-policy rollout kernel (env.rollout_random: k env steps per launch, every env's
+    per-step reward and done flag recorded in (k, E) buffers), `steps` env steps from the restored state, median of 3;
+    `gather` (config 5, N > 1): the episode-stats gather once per rollout segment."""
+    import torch
+
+    E = env.num_envs
+    rew = torch.empty((k, E), dtype=torch.float64, device=device)
+    dn = torch.empty((k, E), dtype=torch.uint8, device=device)
+
+    def seg(ev):
+        env.rollout_random(k, seed, None, rew, dn)
+        if gather is not None:
+            gather()
+
+    n = max(steps // k, 2)
+    dt, _ = timed_loop(seg, n, 0, pg, device, reps=3, prepare=restore)
+    return world * E * n * k / dt
 
 
 def windy_ca_only(env, K, W, pg, device):
