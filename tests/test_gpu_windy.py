@@ -342,8 +342,9 @@ def test_rollout_random_equals_step_random(device, N, K):
     assert torch.equal(a_out, torch.stack(acts))
     assert torch.equal(torch.nan_to_num(r_out), torch.nan_to_num(torch.stack(rews)))
     assert torch.equal(d_out, torch.stack(dones))
-    if K > 1:
-        assert int(envs[1].steps_elapsed.sum()) > 0 and int(envs[1].done[4:16].sum()) > 0  # burn-outs happened
+    assert int(envs[1].steps_elapsed.sum()) >= K * (E - 4)
+    if K >= 40:  # at 256^2 the single fires burn out within the rollout (~3 CA steps)
+        assert int(envs[1].done[4:16].sum()) > 0
     before = [t.clone() for t in (envs[1].accu, envs[1].rng_step)]
     envs[1].rollout_random(0, 9)  # K = 0: nothing changes
     assert torch.equal(before[0], envs[1].accu) and torch.equal(before[1], envs[1].rng_step)
