@@ -13,6 +13,9 @@ checked against the reference's own behaviour, quirks and all:
   reset observation: advanced_bulldozer.py:401-411 applies grid_to_rgb_with_extensions to the raw
       (H, W) grid; numpy broadcasting of the same expressions reproduces what JAX computes.
 Colours: advanced_bulldozer.py:41-60 (PIL ImageColor of the hex strings).
+Pinned (r06) to the reference EXECUTING: tests/golden/observation.npz holds the reference's own builders run as published
+under a numpy stand-in for jax (tests/golden/_jax_standin.py); tests/test_observation_golden.py checks this restatement
+against it bit for bit.
 """
 import numpy as np
 
