@@ -32,6 +32,15 @@ Fixture inventory:
                    use numpy and the global legacy np.random state only; the module's own
                    `import jax.numpy` / `from flax import struct` lines get empty stand-in
                    modules here (jax and flax are not installed).
+  alexandridis_jax.npz
+                   PartiallyObservableForestFireJax.update   ca_alexandridis_jax.py:54-460, the headline rule
+                   EXECUTED as published under tests/golden/_jax_standin.py (numpy with jax's x64-disabled
+                   dtype rules for jnp; jit = identity; vmap = a loop over in_axes; lax.dynamic_slice; random
+                   draws logged in call order): 4 cases, 2-4 chained steps, every random array the rule
+                   consumed, its burn probabilities and outputs (grid, fire_age, wind_index).
+  observation.npz  MDP.build_observation_on_extensions / grid_to_rgb_with_extensions / grid_to_rgb
+                   (advanced_bulldozer.py:988-1101) with extension_utils.py:89-196, executed the same way:
+                   36 cases, the step frame, the channel stack and (square grids) the reset frame.
 
 Usage:  python tests/golden/make_golden.py [fixture ...]   (default: all)
 """
