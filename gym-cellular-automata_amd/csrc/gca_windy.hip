@@ -751,17 +751,22 @@ __global__ __launch_bounds__(256) void bulldozer_step_fused_parts_kernel(
 // gca_bulldozer_step_fused_random (tests/test_gpu_windy.py). Workgroups never wait for each other, so an env whose fire
 // burns out or whose CA steps are few runs ahead: the K x E env steps cost the slowest env's chain, not K launches of
 // the slowest step. Per-step outputs (optional): the actions (K, E, 2), rewards (K, E) and done flags (K, E).
-template <int NW, bool STD>
+// SOLO (the host proves that no cell is modified twice without a CA step between: effect[effect[v]] < 0 or
+// effect[effect[v]] == effect[v] for every v with effect[v] >= 0 -- the bulldozer's {TREE: EMPTY}): every thread applies
+// Modify itself, the same byte to the same cell, and so sees its own writes in program order; a wave that runs ahead
+// only ever meets another wave's late write of the value it wrote itself. Then a step without a CA pass needs no
+// barrier at all (one per CA step remains); otherwise thread 0 applies Modify and broadcasts through LDS behind a
+// barrier per step.
+template <int NW, bool STD, bool SOLO>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) void bulldozer_rollout_random_kernel(
     gca_bulldozer_params p, int K, uint64_t seed, int32_t* __restrict__ action_out, double* __restrict__ reward_out,
     uint8_t* __restrict__ done_out, double* __restrict__ accu, int32_t* __restrict__ steps, uint8_t* __restrict__ done,
     const double* __restrict__ wind, int64_t wind_stride, uint32_t* __restrict__ rng_step, uint8_t* __restrict__ parity,
-    uint8_t* __restrict__ buf0, uint8_t* __restrict__ buf1, int H, int32_t* __restrict__ pos,
-    int32_t* __restrict__ counts, uint8_t* __restrict__ hit, double* __restrict__ reward,
-    int64_t* __restrict__ steps_elapsed, int E) {
+    uint8_t* buf0, uint8_t* buf1, int H, int32_t* __restrict__ pos, int32_t* __restrict__ counts,
+    uint8_t* __restrict__ hit, double* __restrict__ reward, int64_t* __restrict__ steps_elapsed, int E) {
     constexpr int W = 256 * NW;
-    __shared__ int32_t wave_cnt[16][3];
-    __shared__ int32_t bc[2][4];  // thread 0 -> the workgroup, per step (double-buffered): E, T, F counts, hit
+    __shared__ int32_t wave_cnt[2][16][3];  // per CA step, double-buffered (no barrier after the counts are read)
+    __shared__ int32_t bc[2][4];  // !SOLO: thread 0 -> the workgroup, per step (double-buffered): E, T, F counts, hit
     const int e = blockIdx.x;
     const int tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, nw = (int)(blockDim.x >> 6);
@@ -775,7 +780,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
     int64_t se = steps_elapsed ? steps_elapsed[e] : 0;
     uint8_t h = hit[e];
     double rew = reward[e];
-    int last_n = 0;
+    int last_n = 0, ca = 0;
     double wl[9];
 #pragma unroll
     for (int k = 0; k < 9; ++k) wl[k] = wind[(int64_t)e * wind_stride + k];
@@ -807,8 +812,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
         uint8_t* grid = (odd ? buf1 : buf0) + e * HW;
         if (n > 0) {
             auto get_mask = [&]() -> uint32_t { return wave_windy_mask(p, wl, e, rs, lane); };
-            const uint8_t* __restrict__ S = grid;
-            uint8_t* __restrict__ Dst = (odd ? buf0 : buf1) + e * HW;
+            const uint8_t* S = grid;
+            uint8_t* Dst = (odd ? buf0 : buf1) + e * HW;
             int32_t cntT = 0, cntF = 0, cntV = 0;
             for (int s0 = wave * FUSED_SH<NW>; s0 < H; s0 += nw * FUSED_SH<NW>)
                 windy_rows_strip_f<NW, FUSED_SH<NW>, FUSED_RD<NW>, STD>(S, Dst, s0, H, get_mask, lofs, rep4(p.empty),
@@ -819,26 +824,28 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
                 cntF += __shfl_xor(cntF, off);
                 cntV += __shfl_xor(cntV, off);
             }
+            int32_t (*WC)[3] = wave_cnt[ca & 1];  // a wave that runs ahead writes the other buffer at the next CA step
+            ++ca;
             if (lane == 0) {
-                wave_cnt[wave][0] = cntV - cntT - cntF;
-                wave_cnt[wave][1] = cntT;
-                wave_cnt[wave][2] = cntF;
+                WC[wave][0] = cntV - cntT - cntF;
+                WC[wave][1] = cntT;
+                WC[wave][2] = cntF;
             }
             __syncthreads();  // the new grid (every wave's stores) and the counts are complete
             grid = Dst;
             odd = !odd;
             cE = cT = cF = 0;
             for (int w = 0; w < nw; ++w) {
-                cE += wave_cnt[w][0];
-                cT += wave_cnt[w][1];
-                cF += wave_cnt[w][2];
+                cE += WC[w][0];
+                cT += WC[w][1];
+                cF += WC[w][2];
             }
         }
         acc = x - reps;
         row = nrow;
         col = ncol;
-        int32_t* B = bc[k & 1];
-        if (tid == 0) {  // MoveModify (move_modify.py:128-134): Modify at the new position, on the post-CA grid
+        // MoveModify (move_modify.py:128-134): Modify at the new position, on the post-CA grid
+        auto modify = [&](int32_t& mE, int32_t& mT, int32_t& mF) -> uint8_t {
             uint8_t hh = 0;
             if (act1 && row >= 0 && row < H && col >= 0 && col < W) {
                 const int v = grid[(int64_t)row * W + col];
@@ -848,20 +855,29 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
                     hh = 1;
                     const int c_old = cell_category(v, p.empty, p.tree, p.fire);
                     const int c_new = cell_category(nv, p.empty, p.tree, p.fire);
-                    if (c_old == 0) cE -= 1; else if (c_old == 1) cT -= 1; else if (c_old == 2) cF -= 1;
-                    if (c_new == 0) cE += 1; else if (c_new == 1) cT += 1; else if (c_new == 2) cF += 1;
+                    if (c_old == 0) mE -= 1; else if (c_old == 1) mT -= 1; else if (c_old == 2) mF -= 1;
+                    if (c_new == 0) mE += 1; else if (c_new == 1) mT += 1; else if (c_new == 2) mF += 1;
                 }
             }
-            B[0] = cE;
-            B[1] = cT;
-            B[2] = cF;
-            B[3] = hh;
+            return hh;
+        };
+        if constexpr (SOLO) {
+            h = modify(cE, cT, cF);
+        } else {
+            int32_t* B = bc[k & 1];
+            if (tid == 0) {
+                const uint8_t hh = modify(cE, cT, cF);
+                B[0] = cE;
+                B[1] = cT;
+                B[2] = cF;
+                B[3] = hh;
+            }
+            __syncthreads();  // the Modify write and its counts, for every wave's next step
+            cE = B[0];
+            cT = B[1];
+            cF = B[2];
+            h = (uint8_t)B[3];
         }
-        __syncthreads();  // the Modify write and its counts, for every wave's next step
-        cE = B[0];
-        cT = B[1];
-        cF = B[2];
-        h = (uint8_t)B[3];
         rew = (cT + cF) > 0 ? -((double)cF / (double)(cT + cF)) : (double)NAN;
         was_done = cF == 0;
         rs += (uint32_t)n;
@@ -1072,14 +1088,24 @@ extern "C" int gca_bulldozer_rollout_random(const gca_bulldozer_params* p, uint6
     const int threads = 64 * (strips < 16 ? strips : 16);
     hipStream_t st = (hipStream_t)stream;
     const bool std_codes = p->empty == 0 && p->tree == 3 && p->fire == 25;
-#define GCA_ROLLOUT_LAUNCH(NWV, STDV)                                                                                    \
-    hipLaunchKernelGGL((bulldozer_rollout_random_kernel<NWV, STDV>), dim3((unsigned)E), dim3(threads), 0, st, *p, K,    \
-                       action_seed, action_out, reward_out, done_out, accu, steps, done, wind, wind_stride, rng_step,     \
+    // SOLO: no cell is modified twice without a CA step between (the kernel's comment)
+    bool solo = true;
+    for (int v = 0; v < 256; ++v) {
+        const int nv = p->effect[v];
+        if (nv >= 0 && nv < 256 && p->effect[nv] >= 0 && p->effect[nv] != nv) solo = false;
+    }
+#define GCA_ROLLOUT_LAUNCH(NWV, STDV, SOLOV)                                                                             \
+    hipLaunchKernelGGL((bulldozer_rollout_random_kernel<NWV, STDV, SOLOV>), dim3((unsigned)E), dim3(threads), 0, st, *p, \
+                       K, action_seed, action_out, reward_out, done_out, accu, steps, done, wind, wind_stride, rng_step,  \
                        parity, buf0, buf1, H, pos, counts, hit, reward, steps_elapsed, E)
     if (W == 256) {
-        if (std_codes) GCA_ROLLOUT_LAUNCH(1, true); else GCA_ROLLOUT_LAUNCH(1, false);
+        if (std_codes && solo) GCA_ROLLOUT_LAUNCH(1, true, true);
+        else if (solo) GCA_ROLLOUT_LAUNCH(1, false, true);
+        else GCA_ROLLOUT_LAUNCH(1, false, false);
     } else {
-        if (std_codes) GCA_ROLLOUT_LAUNCH(2, true); else GCA_ROLLOUT_LAUNCH(2, false);
+        if (std_codes && solo) GCA_ROLLOUT_LAUNCH(2, true, true);
+        else if (solo) GCA_ROLLOUT_LAUNCH(2, false, true);
+        else GCA_ROLLOUT_LAUNCH(2, false, false);
     }
 #undef GCA_ROLLOUT_LAUNCH
     GCA_CHECK_LAUNCH("bulldozer_rollout_random");

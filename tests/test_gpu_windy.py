@@ -296,11 +296,14 @@ def test_step_random_graph_replay_equals_eager(device, N, G):
     assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
 
 
-@pytest.mark.parametrize("N,K", [(256, 40), (512, 24), (256, 1)])
-def test_rollout_random_equals_step_random(device, N, K):
+@pytest.mark.parametrize("N,K,chain", [(256, 40, False), (512, 24, False), (256, 1, False), (256, 40, True),
+                                       (512, 16, True)])
+def test_rollout_random_equals_step_random(device, N, K, chain):
     """gca_bulldozer_rollout_random (env.rollout_random): K env steps in one launch equal K env.step_random calls bit
     for bit -- every state tensor after the rollout, and the per-step actions, rewards and done flags against each
-    step's own -- from a state where some envs burn out during the rollout and some are finished before it."""
+    step's own -- from a state where some envs burn out during the rollout and some are finished before it. chain: a
+    Modify effect that can modify a cell twice in a row (TREE -> FIRE -> EMPTY), which takes the kernel's
+    barrier-per-step path instead of the SOLO one."""
     import torch
 
     from gymca_amd import _device as dev
@@ -311,6 +314,8 @@ def test_rollout_random_equals_step_random(device, N, K):
     envs = [BatchedForestFireBulldozerEnv(E, N, N, device=device, seed=31, env_offset=3, materialize_obs=False)
             for _ in range(2)]
     for env in envs:
+        if chain:
+            env.params.effect[3], env.params.effect[25] = 25, 0
         env.reset(seed=7)
         _dense_state(env, device, seed=5, p_fire=0.05)
         g = env.grids()
