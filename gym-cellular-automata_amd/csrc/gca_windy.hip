@@ -751,12 +751,13 @@ __global__ __launch_bounds__(256) void bulldozer_step_fused_parts_kernel(
 // gca_bulldozer_step_fused_random (tests/test_gpu_windy.py). Workgroups never wait for each other, so an env whose fire
 // burns out or whose CA steps are few runs ahead: the K x E env steps cost the slowest env's chain, not K launches of
 // the slowest step. Per-step outputs (optional): the actions (K, E, 2), rewards (K, E) and done flags (K, E).
-// SOLO (the host proves that no cell is modified twice without a CA step between: effect[effect[v]] < 0 or
-// effect[effect[v]] == effect[v] for every v with effect[v] >= 0 -- the bulldozer's {TREE: EMPTY}): every thread applies
-// Modify itself, the same byte to the same cell, and so sees its own writes in program order; a wave that runs ahead
-// only ever meets another wave's late write of the value it wrote itself. Then a step without a CA pass needs no
-// barrier at all (one per CA step remains); otherwise thread 0 applies Modify and broadcasts through LDS behind a
-// barrier per step.
+// SOLO (the host proves that Modify never changes the FIRE count: no effect maps a FIRE cell or onto FIRE -- the
+// bulldozer's {TREE: EMPTY}): thread 0 alone applies Modify and keeps the E / T counts, hit and reward; every other
+// thread needs only the FIRE count (done), which then changes only in CA steps, whose counts all threads sum. A step
+// without a CA pass needs no barrier at all; a CA step opens with one (thread 0's Modify writes since the last barrier,
+// before the other waves' CA reads) and closes with one (the new grid and the counts). Otherwise thread 0 applies
+// Modify and broadcasts its counts through LDS behind a barrier per step. (Every thread applying Modify itself was
+// tried first: a slow wave then reads the cell a fast wave already rewrote and miscounts, r06f.)
 template <int NW, bool STD, bool SOLO>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) void bulldozer_rollout_random_kernel(
     gca_bulldozer_params p, int K, uint64_t seed, int32_t* __restrict__ action_out, double* __restrict__ reward_out,
@@ -811,6 +812,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
         move_pos(a0, nrow, ncol, H, W, p.up_mask, p.down_mask, p.left_mask, p.right_mask);
         uint8_t* grid = (odd ? buf1 : buf0) + e * HW;
         if (n > 0) {
+            if constexpr (SOLO) __syncthreads();  // thread 0's Modify writes since the last barrier, before the CA reads
             auto get_mask = [&]() -> uint32_t { return wave_windy_mask(p, wl, e, rs, lane); };
             const uint8_t* S = grid;
             uint8_t* Dst = (odd ? buf0 : buf1) + e * HW;
@@ -862,7 +864,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
             return hh;
         };
         if constexpr (SOLO) {
-            h = modify(cE, cT, cF);
+            if (tid == 0) h = modify(cE, cT, cF);  // FIRE count unchanged (host-checked): the other threads' cF holds
         } else {
             int32_t* B = bc[k & 1];
             if (tid == 0) {
@@ -1088,11 +1090,12 @@ extern "C" int gca_bulldozer_rollout_random(const gca_bulldozer_params* p, uint6
     const int threads = 64 * (strips < 16 ? strips : 16);
     hipStream_t st = (hipStream_t)stream;
     const bool std_codes = p->empty == 0 && p->tree == 3 && p->fire == 25;
-    // SOLO: no cell is modified twice without a CA step between (the kernel's comment)
+    // SOLO: Modify never changes the FIRE count (the kernel's comment)
     bool solo = true;
+    auto fire_cat = [&](int v) { return v == p->fire; };
     for (int v = 0; v < 256; ++v) {
         const int nv = p->effect[v];
-        if (nv >= 0 && nv < 256 && p->effect[nv] >= 0 && p->effect[nv] != nv) solo = false;
+        if (nv >= 0 && fire_cat(v) != fire_cat(nv)) solo = false;
     }
 #define GCA_ROLLOUT_LAUNCH(NWV, STDV, SOLOV)                                                                             \
     hipLaunchKernelGGL((bulldozer_rollout_random_kernel<NWV, STDV, SOLOV>), dim3((unsigned)E), dim3(threads), 0, st, *p, \
