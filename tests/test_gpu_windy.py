@@ -348,7 +348,7 @@ def test_rollout_random_equals_step_random(device, N, K, chain):
     assert torch.equal(torch.nan_to_num(r_out), torch.nan_to_num(torch.stack(rews)))
     assert torch.equal(d_out, torch.stack(dones))
     assert int(envs[1].steps_elapsed.sum()) >= K * (E - 16)  # envs 4..15 may burn out during the rollout
-    if K >= 40:  # at 256^2 the single fires burn out within the rollout (~3 CA steps)
+    if K >= 40 and not chain:  # at 256^2 the single fires burn out within the rollout (~3 CA steps)
         assert int(envs[1].done[4:16].sum()) > 0
     before = [t.clone() for t in (envs[1].accu, envs[1].rng_step)]
     envs[1].rollout_random(0, 9)  # K = 0: nothing changes
