@@ -542,9 +542,9 @@ def bench_windy(args, world, rank, device, pg):
         graphs[name] = world * E * reps_g * g_steps / dtg
         del graph
     best_graph = max(graphs, key=graphs.get)
-    # the same random policy, 32 env steps per launch (gca_bulldozer_rollout_random: the env's state in registers across
-    # the steps), the per-step rewards and done flags recorded
-    rollout = rollout_rate(env, 9, max(Kg * G // 32, 2) * 32, restore, pg, device, world)
+    # the same random policy, 32 / 128 env steps per launch (gca_bulldozer_rollout_random: the env's state in registers
+    # across the steps), the per-step rewards and done flags recorded
+    rollout = {f"k{k}": rollout_rate(env, 9, max(Kg * G // k, 2) * k, restore, pg, device, world, k=k) for k in (32, 128)}
     # CA-only (steps[E] = 1 forced), dense variant {0:.1, 3:.6, 25:.3}
     g = env.grids()
     u = torch.rand(g.shape, device=device)
@@ -588,7 +588,8 @@ def bench_windy(args, world, rank, device, pg):
         "env_steps_per_s_eager": world * E * Kg * G / dt_eager,
         "env_steps_per_s_random_policy_fused": world * E * Kg * G / dt_rand,
         "env_steps_per_s_graphs": graphs,
-        "env_steps_per_s_rollout_random_k32": rollout,
+        # the random policy's K-step rollouts, K = 32 / 128 env steps per launch (a PPO-style rollout length)
+        "env_steps_per_s_rollout_random": rollout,
         "loops": f"eager, random-policy-fused and the graphs: the same {Kg * G} env steps (graphs: whole graphs, at "
                  f"least 2) from one mid-episode state (reset + 64 steps, restored before each repetition), median of 3",
         "env_step_graph": "hipGraph of env steps: sample_step_g8 = 8 x (gca_random_actions + gca_bulldozer_step_fused), "
@@ -667,7 +668,8 @@ def bench_windy512(args, world, rank, device, pg):
         graphs[name] = world * E * reps_g * g_steps / dtg
         del graph
     best_graph = max(graphs, key=graphs.get)
-    rollout = rollout_rate(env, 11, max(K // 32, 2) * 32, restore, pg, device, world, gather=gather)
+    rollout = {f"k{k}": rollout_rate(env, 11, max(K // k, 2) * k, restore, pg, device, world, k=k, gather=gather)
+               for k in (32, 128)}
     check = gd.verify_gather(stats)
     # CA-only at HBM scale: one forced Windy step of every env, 268 MB per buffer (beyond the 256 MB
     # Infinity Cache, unlike config 2's 64 MiB pair), dense {0:.1, 3:.6, 25:.3}, beside a same-size copy
@@ -676,7 +678,8 @@ def bench_windy512(args, world, rank, device, pg):
             "env_steps_per_s": graphs[best_graph],
             "env_steps_per_s_path": best_graph + " (graph segment + one gather per segment)",
             "env_steps_per_s_graphs": graphs,
-            "env_steps_per_s_rollout_random_k32": rollout,
+            # the random policy's K-step rollouts, K = 32 / 128 env steps per launch (a PPO-style rollout length)
+        "env_steps_per_s_rollout_random": rollout,
             "env_step": ("gca_bulldozer_step_fused (one launch per env step)" if env.fused else
                          "pre / Windy passes / post kernels"),
             "env_steps_per_s_eager_gather_every_step": world * E * K / dt_eager,
