@@ -678,8 +678,7 @@ def bench_windy512(args, world, rank, device, pg):
             "env_steps_per_s": graphs[best_graph],
             "env_steps_per_s_path": best_graph + " (graph segment + one gather per segment)",
             "env_steps_per_s_graphs": graphs,
-            # the random policy's K-step rollouts, K = 32 / 128 env steps per launch (a PPO-style rollout length)
-        "env_steps_per_s_rollout_random": rollout,
+            "env_steps_per_s_rollout_random": rollout,  # K = 32 / 128 env steps per launch, one gather per rollout
             "env_step": ("gca_bulldozer_step_fused (one launch per env step)" if env.fused else
                          "pre / Windy passes / post kernels"),
             "env_steps_per_s_eager_gather_every_step": world * E * K / dt_eager,
