@@ -177,8 +177,8 @@ class BatchedForestFireBulldozerEnv:
         into the env's action buffer."""
         import torch
 
-        if (type(action) is torch.Tensor and action.dtype == torch.int32 and action.shape == self._act_shape
-                and action.device == self.device and action.is_contiguous()):
+        if (type(action) is torch.Tensor and action.dtype is torch.int32 and action.get_device() == self._dev_index
+                and action.shape == self._act_shape and action.is_contiguous()):
             return action
         src = action if dev.is_device_tensor(action) else torch.as_tensor(np.asarray(action))
         self._act_buf.copy_(src.reshape(self.num_envs, 2))
@@ -225,8 +225,8 @@ class BatchedForestFireBulldozerEnv:
         import torch
 
         out = self._act_buf if action_out is None else action_out
-        if not (type(out) is torch.Tensor and out.dtype == torch.int32 and out.shape == self._act_shape
-                and out.device == self.device and out.is_contiguous()):
+        if not (type(out) is torch.Tensor and out.dtype is torch.int32 and out.get_device() == self._dev_index
+                and out.shape == self._act_shape and out.is_contiguous()):
             raise ValueError("step_random: action_out must be a contiguous int32 (E, 2) tensor on the env's device")
         key = (seed, out.data_ptr())
         rc = self._random_call
@@ -277,8 +277,8 @@ class BatchedForestFireBulldozerEnv:
         import torch
 
         out = self._act_buf if out is None else out
-        if not (type(out) is torch.Tensor and out.dtype == torch.int32 and out.shape == self._act_shape
-                and out.device == self.device and out.is_contiguous()):
+        if not (type(out) is torch.Tensor and out.dtype is torch.int32 and out.get_device() == self._dev_index
+                and out.shape == self._act_shape and out.is_contiguous()):
             raise ValueError("sample_actions: out must be a contiguous int32 (E, 2) tensor on the env's device")
         sc = self._sample_call
         if sc is None or sc[0] is not out or sc[1] != tag or sc[2] != out.data_ptr():
