@@ -25,6 +25,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "gym-cellular-automata_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
 
 
@@ -68,6 +69,42 @@ def main():
         for kind in rates:
             rates[kind].append(leg(kind, args.seconds))
     med = {k: sorted(v)[len(v) // 2] for k, v in rates.items()}
+
+    # the bulldozer env loop, 256^2, random actions: the reference's ForestFireBulldozerEnv (with the {"wind": W}
+    # unwrap make_golden.py applies) against bench.py's restated loop (oracle.windy.BulldozerOracle +
+    # the Counter count), env-steps/s
+    import bench
+    from gymca_amd.forest_fire.bulldozer.bulldozer import DEFAULT_WIND, bulldozer_timings, parse_wind  # noqa: F401
+
+    orig = R.windy.WindyForestFire.update
+
+    def patched(self, grid, action, wind):
+        if isinstance(wind, dict):
+            g, _ = orig(self, grid, action, wind["wind"])
+            return g, wind
+        return orig(self, grid, action, wind)
+
+    def ref_env_leg(seconds):
+        R.windy.WindyForestFire.update = patched
+        try:
+            env = R.bd.ForestFireBulldozerEnv(256, 256)
+            env.reset(seed=1)
+            arng = np.random.default_rng(3)
+            steps, t0 = 0, time.perf_counter()
+            while time.perf_counter() - t0 < seconds:
+                _, _, term, _, _ = env.step(np.array([arng.integers(0, 9), arng.integers(0, 2)]))
+                steps += 1
+                if term:
+                    env.reset()
+            return steps / (time.perf_counter() - t0)
+        finally:
+            R.windy.WindyForestFire.update = orig
+
+    env_rates = {"ref": [], "port": []}
+    for _ in range(args.passes):
+        env_rates["ref"].append(ref_env_leg(args.seconds))
+        env_rates["port"].append(bench.bulldozer_cpu_baseline(args.seconds)["value"])
+    env_med = {k: sorted(v)[len(v) // 2] for k, v in env_rates.items()}
     out = {"what": "WindyForestFire 256x256 step + cell count, one core, cell-updates/s (median of interleaved passes)",
            "reference": "ca_windy.py WindyForestFire.update (its own np_random roll) + Counter count (ca_env.py:94-99)",
            "port": "oracle/windy.py windy_step (scipy convolve2d restatement) + the same Counter count",
@@ -75,6 +112,12 @@ def main():
            "median": med, "passes": rates, "port_over_ref": med["port"] / med["ref"],
            "unique_over_ref": med["unique"] / med["ref"],
            "within_20pct": abs(med["port"] / med["ref"] - 1) <= 0.2,
+           "bulldozer_env_256": {"what": "ForestFireBulldozerEnv 256x256 env loop, random actions, env-steps/s, one core",
+                                 "reference": "bulldozer.py ForestFireBulldozerEnv.step (the {'wind': W} unwrap patch)",
+                                 "port": "bench.py bulldozer_cpu_baseline (oracle/windy.py BulldozerOracle + Counter)",
+                                 "median": env_med, "passes": env_rates,
+                                 "port_over_ref": env_med["port"] / env_med["ref"],
+                                 "within_20pct": abs(env_med["port"] / env_med["ref"] - 1) <= 0.2},
            "seconds_per_pass": args.seconds, "cpu": platform.processor() or platform.machine(),
            "numpy": np.__version__}
     path = os.path.join(ROOT, "profiles", "cpu_crosscheck.json")
