@@ -698,6 +698,50 @@ def bench_windy512(args, world, rank, device, pg):
             "ca_frac_of_same_size_copy": ca["copy_s"] / ca["kernel_s"]}
 
 
+def bench_windy512_strong(args, world, rank, device, pg, total=8192):
+    """BASELINE config 5 as strong scaling: the 8192 envs of 512^2 split over the ranks
+    (distributed.shard; at N = 1 all 8192 on one GPU), the random policy through a hipGraph of 8 step_random steps with
+    one episode-stats gather per graph, and the 128-step rollout kernel with one gather per rollout. Rates are whole-job
+    env-steps/s (the sum of every rank's envs over the max-over-ranks time)."""
+    import torch
+
+    from gymca_amd import distributed as gd
+    from gymca_amd.forest_fire.bulldozer import BatchedForestFireBulldozerEnv
+    from gymca_amd.graph import StepGraph
+
+    N = 512
+    off, E = gd.shard(total, world, rank)
+    env = BatchedForestFireBulldozerEnv(E, N, N, device=device, seed=0x5EED5, env_offset=off, materialize_obs=False)
+    env.reset()
+    action = torch.zeros((E, 2), dtype=torch.int32, device=device)
+    stats = gd.StatsGather(E, device, len_dtype=env.steps_elapsed.dtype) if world > 1 else None
+
+    def gather():
+        if stats is not None:
+            stats.gather(env.done, env.reward, env.steps_elapsed)
+
+    restore = env_snapshot(env, lambda: env.step(env.sample_actions(action, 11)), 32)
+    graph = StepGraph(lambda: env.step_random(11, action), n_steps=8, device=device)
+
+    def seg(ev):
+        graph.replay()
+        gather()
+
+    dt_g, _ = timed_loop(seg, 8, 0, pg, device, reps=3, prepare=restore)
+    del graph
+    roll = rollout_rate(env, 11, 256, restore, pg, device, 1, k=128, gather=gather)  # this rank's envs
+    # whole job: every rank's rollout rate is E_rank x steps / (its time); the job's is total x steps / max time, which
+    # timed_loop's max-over-ranks already gives for the graph; for the rollout use the same total
+    out = {"config": f"ForestFireBulldozer 512x512, {total} envs in all over {world} GPU(s) (strong scaling)",
+           "envs_this_rank": E,
+           "env_steps_per_s_graph_step_random_g8": total * 8 * 8 / dt_g,
+           "env_steps_per_s_rollout_random_k128": roll * total / E,
+           "gather": "one StatsGather all_gather per graph / per rollout" if world > 1 else "none (1 GPU)"}
+    del env
+    torch.cuda.empty_cache()
+    return out
+
+
 def rollout_rate(env, seed, steps, restore, pg, device, world, k=32, gather=None):
     """env-steps/s of the random-policy rollout kernel (env.rollout_random: k env steps per launch, every env's
     per-step reward and done flag recorded in (k, E) buffers), `steps` env steps from the restored state, median of 3;
@@ -1219,6 +1263,7 @@ def main():
     alex512 = None if (args.no_secondary or args.size != 256) else bench_alex512(args, world, rank, device, pg)
     secondary = None if args.no_secondary else bench_windy(args, world, rank, device, pg)
     config5 = None if args.no_secondary else bench_windy512(args, world, rank, device, pg)
+    config5_strong = None if args.no_secondary else bench_windy512_strong(args, world, rank, device, pg)
     # the one-env drop-ins on rank 0 only (no collective inside; the other ranks go on to the copy-rate probe)
     dropins = None if (args.no_secondary or rank != 0) else bench_dropins(device)
     if cpu_legs is not None:
@@ -1303,6 +1348,7 @@ def main():
             "config4": config4,
             "alex_512": alex512,
             "config5": config5,
+            "config5_strong": config5_strong,
             "dropins": dropins,
         }
         print(json.dumps(out))
