@@ -255,7 +255,14 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
     int strips, e, s, g;
     if constexpr (!HALO) {
         const int wv = lb * 4 + wl;
-        if (wv >= nwaves) return;  // wave-uniform; no barrier follows
+        if (wv >= nwaves) {  // wave-uniform; no barrier follows -- but XROW's one barrier per live wave: join it
+            if constexpr (XROW) {
+                if (lane == 0) xok[wl] = 0u;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+                __builtin_amdgcn_s_barrier();
+            }
+            return;
+        }
         strips = H / SH;
         // (env-major wave order: one env's tiles back to back. A tile-major order inside chunks of 128 / 256 / 512
         //  envs, meant to turn the tiles' shared halo rows into L2 hits, measured 5 / 8 / 12 % slower, profiles/r03p)

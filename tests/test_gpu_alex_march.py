@@ -139,6 +139,33 @@ def test_march_tile_skip_and_frame(device):
     assert (got[3][1] == 0).all() and got[3][0].any()
 
 
+@pytest.mark.parametrize("E,H", [(3, 16), (5, 48), (1, 32)])
+def test_march_frame_partial_last_workgroup(device, E, H):
+    """The fused-frame march kernel when the wave count is not a multiple of 4 (the last workgroup's excess waves exit
+    at once and join the XROW barrier): grid, ages, counts and frame equal the tiled kernel's, day and night."""
+    import torch
+
+    from gymca_amd import _device as dev
+    from gymca_amd._lib import call
+    from gymca_amd.forest_fire.bulldozer.observation import make_obs_params
+
+    W = 256
+    case = make_case(E, H, W, 70 + E, p_tree=0.0, dousing_p=0.2, fire_p=0.06)
+    p = params(H, 0.0, seed=4)
+    es, _ = slopes(device, altitude(E, H, W, 70 + E))
+    coal = _coalesced(device, es)
+    vd, bits = _layers(device, case)
+    op = make_obs_params(0, 1, 2, False, False, 8)
+    col = torch.zeros((12, 4), dtype=torch.float32, device=device)
+    call("gca_obs_color_table", op, dev.ptr(col), dev.stream_ptr())
+    night = torch.as_tensor(np.arange(E, dtype=np.int32) % 2, device=device)
+    rs = np.full(E, 5, np.uint32)
+    ref = _run(device, "gca_alex_step_packed_rgb", p, case, coal, rs, vd, bits, rgb=(col, night))
+    got = _run(device, "gca_alex_step_march_rgb", p, case, es, rs, vd, bits, rgb=(col, night))
+    for k in (0, 1, 2, 4):
+        assert np.array_equal(got[k], ref[k]), k
+
+
 def test_march_matches_oracle(device):
     """The marching step against the C oracle (Philox mode) on the unpacked state, directly."""
     E, H, W = 2, 64, 256
