@@ -5,7 +5,10 @@ _compute_pinecone_burn_probability (:208-227) line by line, with the JAX random 
 (n_pinecones, directions, normal thrusts, uniforms), plus the scatter of _update_grid (:400-420,
 commented out in the reference) with the duplicate rule our device kernel defines: a target ignites iff
 any pinecone landing on it burns (the reference's .at[].set leaves duplicate order unspecified); its age
-comes from `target_ages`. Parity unpinned at the reference level (jax absent; the code is disabled there).
+comes from `target_ages`. Pinned (r06) to the reference executing: tests/golden/pinecones_jax.npz holds
+_handle_pinecone_spread run as published under a numpy stand-in for jax (tests/golden/_jax_standin.py), and
+tests/test_pinecones_oracle.py checks the landings and burn mask bit for bit (the scatter :400-420 stays disabled in
+the reference, so its duplicate rule is ours).
 
 `decode_draws` turns the device's Philox convention (gca_pine.hip) into these arrays, so the C oracle /
 device result can be checked against the literal restatement on identical draws.

@@ -38,6 +38,9 @@ Fixture inventory:
                    dtype rules for jnp; jit = identity; vmap = a loop over in_axes; lax.dynamic_slice; random
                    draws logged in call order): 4 cases, 2-4 chained steps, every random array the rule
                    consumed, its burn probabilities and outputs (grid, fire_age, wind_index).
+  pinecones_jax.npz
+                   _handle_pinecone_spread (ca_alexandridis_jax.py:208-319) executed the same way: 4 cases,
+                   the Poisson / direction / thrust / uniform draws and the landings and burn mask.
   observation.npz  MDP.build_observation_on_extensions / grid_to_rgb_with_extensions / grid_to_rgb
                    (advanced_bulldozer.py:988-1101) with extension_utils.py:89-196, executed the same way:
                    36 cases, the step frame, the channel stack and (square grids) the reset frame.
@@ -667,10 +670,52 @@ def gen_observation(R, rng):
     return out
 
 
+def gen_pinecones_jax(R, rng):
+    """PartiallyObservableForestFireJax._handle_pinecone_spread (ca_alexandridis_jax.py:229-319, with
+    _compute_pinecone_burn_probability :208-227) EXECUTED as published under the jax stand-in: the draws it consumed
+    (Poisson counts, directions, normal thrusts, burn uniforms, in call order) and its outputs (flat landing rows /
+    columns and the burn mask). The reference leaves the spotting disabled in _update_grid (:400-420); the fixture pins
+    the function the device's opt-in pinecone pass restates."""
+    sys.path.insert(0, HERE)
+    import _jax_standin as js
+
+    rlog = js.RandomLog(np.random.default_rng(0))
+    with js.installed(rlog):
+        aj = _load("gym_cellular_automata.forest_fire.operators.ca_alexandridis_jax",
+                   f"{REF}/forest_fire/operators/ca_alexandridis_jax.py")
+        iu = _load("gym_cellular_automata.forest_fire.bulldozer.utils.init_utils",
+                   f"{REF}/forest_fire/bulldozer/utils/init_utils.py")
+        op = aj.PartiallyObservableForestFireJax(256, 0, 1, 2)
+    winds = np.asarray(iu.get_winds(True), dtype=np.float32)
+    wrap = js.wrap
+    out = {}
+    cases = [(16, 16, 0.3), (24, 40, 0.15), (64, 64, 0.05), (7, 5, 0.5)]
+    for ci, (H, W, ff) in enumerate(cases):
+        crng = np.random.default_rng(8800 + ci)
+        old = crng.choice([0, 1, 2], size=(H, W), p=[0.2, 0.8 - ff, ff])
+        new = np.where(old == 2, crng.choice([0, 2], size=(H, W)), crng.choice([0, 1, 2], size=(H, W), p=[0.1, 0.8, 0.1]))
+        veg, den = crng.integers(0, 7, (H, W)), crng.integers(0, 7, (H, W))
+        ft = winds[ci % 8, 1]
+        ctx = {"current_ft": wrap(ft), "vegetation": wrap(veg), "density": wrap(den)}
+        rlog.gen = np.random.default_rng(9900 + ci)
+        rlog.log.clear()
+        rows, cols, burn = op._handle_pinecone_spread(wrap(new), ("key", ci), ctx, wrap(old == 2))
+        kinds = [k for k, *_ in rlog.log]
+        assert kinds == ["poisson", "randint", "normal", "uniform"], kinds
+        pre = f"c{ci}_"
+        out.update({pre + "old": old.astype(np.uint8), pre + "new": new.astype(np.uint8), pre + "veg": veg.astype(np.uint8),
+                    pre + "den": den.astype(np.uint8), pre + "ft": ft, pre + "n": rlog.log[0][2],
+                    pre + "dirs": rlog.log[1][2], pre + "normal": rlog.log[2][2], pre + "u": rlog.log[3][2],
+                    pre + "rows": np.asarray(rows), pre + "cols": np.asarray(cols),
+                    pre + "burn": np.asarray(burn).astype(np.uint8)})
+    out["n"] = np.array(len(cases))
+    return out
+
+
 GENERATORS = {"windy": gen_windy, "repeat_ca": gen_repeat, "move_modify": gen_move_modify, "bulldozer": gen_bulldozer,
               "drossel": gen_drossel, "helicopter": gen_helicopter, "moore": gen_moore, "init_utils": gen_init_utils,
               "alexandridis_classic": gen_alexandridis_classic, "alexandridis_jax": gen_alexandridis_jax,
-              "observation": gen_observation}
+              "observation": gen_observation, "pinecones_jax": gen_pinecones_jax}
 
 
 def main():

@@ -80,3 +80,21 @@ def test_oracle_pass_matches_literal_restatement(E, H, W, seed):
         ignited += int((want_g != g1[e]).sum())
         assert co[e, 2] - c1[e, 2] == int((want_g != g1[e]).sum()) == c1[e, 1] - co[e, 1]
     assert ignited > 0
+
+
+def test_restatement_reproduces_reference_run(golden):
+    """oracle.pinecones_ref.handle_pinecone_spread against the reference's own _handle_pinecone_spread executed under
+    the jax stand-in (tests/golden/pinecones_jax.npz, make_golden.py::gen_pinecones_jax): the same landings (rows,
+    columns) and burn mask, bit for bit, from the draws the reference consumed."""
+    d = golden("pinecones_jax")
+    landed = burned = 0
+    for ci in range(int(d["n"])):
+        p = f"c{ci}_"
+        rows, cols, burn = ref.handle_pinecone_spread(
+            d[p + "new"].astype(np.int64), d[p + "old"] == 2, d[p + "n"], d[p + "dirs"].astype(np.int64), d[p + "normal"],
+            d[p + "u"], d[p + "veg"].astype(np.int64), d[p + "den"].astype(np.int64), d[p + "ft"], tree=1)
+        assert np.array_equal(rows, d[p + "rows"]) and np.array_equal(cols, d[p + "cols"]), ci
+        assert np.array_equal(burn.astype(np.uint8), d[p + "burn"]), ci
+        landed += int((d[p + "old"] == 2).sum())
+        burned += int(d[p + "burn"].sum())
+    assert landed > 50 and burned > 5
