@@ -247,7 +247,8 @@ def _make_jnp():
         f = getattr(np, name)
 
         def g(*a, **k):
-            return wrap(f(*[_canon(x) if isinstance(x, np.ndarray) else x for x in a], **k))
+            r = f(*[_canon(x) if isinstance(x, np.ndarray) else x for x in a], **k)
+            return tuple(wrap(x) for x in r) if isinstance(r, tuple) else wrap(r)
 
         g.__name__ = name
         return g
@@ -258,7 +259,8 @@ def _make_jnp():
     for name in ("exp", "log", "sqrt", "round", "minimum", "maximum", "max", "min", "sum", "any", "all", "argmax",
                  "abs", "floor", "ceil", "mean", "logical_and", "logical_or", "logical_not", "ones_like",
                  "concatenate", "repeat", "tile", "transpose", "expand_dims", "roll", "sign", "cos", "sin",
-                 "arctan2", "arctan", "degrees", "radians", "cumsum", "einsum", "flip", "isclose", "diff"):
+                 "arctan2", "arctan", "degrees", "radians", "cumsum", "einsum", "flip", "isclose", "diff", "modf", "take",
+                 "invert", "full_like", "trunc", "count_nonzero", "unique"):
         setattr(jnp, name, passthrough(name))
     for name in ("float32", "int32", "uint8", "uint32", "int8", "int16", "bool_", "pi", "newaxis", "ndarray",
                  "issubdtype", "integer", "floating", "inf", "nan"):
@@ -275,6 +277,13 @@ def jit(fun=None, **_):
 
 
 def _take(a, axis, i):
+    """Index i of `a` along `axis`; `axis` may be a pytree prefix of `a` (a dict / tuple of axes, None = unmapped)."""
+    if axis is None:
+        return a
+    if isinstance(axis, dict):
+        return {k: _take(v, axis.get(k), i) for k, v in a.items()}
+    if isinstance(axis, (tuple, list)):
+        return type(a)(_take(x, ax, i) for x, ax in zip(a, axis))
     if isinstance(a, (tuple, list)):
         return type(a)(_take(x, axis, i) for x in a)
     if isinstance(a, dict):
@@ -282,12 +291,18 @@ def _take(a, axis, i):
     return wrap(np.take(np.asarray(a), i, axis=axis))
 
 
-def _size(a, axis):
+def _sizes(a, axis):
+    if axis is None:
+        return set()
+    if isinstance(axis, dict):
+        return set().union(*[_sizes(v, axis.get(k)) for k, v in a.items()])
+    if isinstance(axis, (tuple, list)):
+        return set().union(*[_sizes(x, ax) for x, ax in zip(a, axis)])
     if isinstance(a, (tuple, list)):
-        return _size(a[0], axis)
+        return set().union(*[_sizes(x, axis) for x in a])
     if isinstance(a, dict):
-        return _size(next(iter(a.values())), axis)
-    return np.shape(a)[axis]
+        return set().union(*[_sizes(v, axis) for v in a.values()])
+    return {np.shape(a)[axis]}
 
 
 def _stack_tree(outs):
@@ -304,8 +319,8 @@ def vmap(fun, in_axes=0, out_axes=0):
 
     def mapped(*args):
         axes = tuple(in_axes) if isinstance(in_axes, (tuple, list)) else (in_axes,) * len(args)
-        n = {_size(a, ax) for a, ax in zip(args, axes) if ax is not None}
-        assert len(n) == 1, "vmap: mapped axes differ in size"
+        n = set().union(*[_sizes(a, ax) for a, ax in zip(args, axes)])
+        assert len(n) == 1, f"vmap: mapped axes differ in size {n}"
         outs = [fun(*[a if ax is None else _take(a, ax, i) for a, ax in zip(args, axes)]) for i in range(n.pop())]
         return _stack_tree(outs)
 
@@ -347,10 +362,15 @@ class RandomLog:
 
     def key(self, seed=0):
         self._k += 1
-        return ("key", self._k)
+        return wrap(np.array([self._k, 0], dtype=np.uint32))
 
     def split(self, key, num=2):
-        return [self.key() for _ in range(num)]
+        """An array of `num` fresh key tokens, shape (num, 2) like jax's keys (rows unpack and vmap like them)."""
+        rows = []
+        for _ in range(num):
+            self._k += 1
+            rows.append((self._k, 0))
+        return wrap(np.array(rows, dtype=np.uint32))
 
     def uniform(self, key, shape=(), dtype=None, minval=0.0, maxval=1.0):
         shape = tuple(shape)

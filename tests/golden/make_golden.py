@@ -44,6 +44,11 @@ Fixture inventory:
   observation.npz  MDP.build_observation_on_extensions / grid_to_rgb_with_extensions / grid_to_rgb
                    (advanced_bulldozer.py:988-1101) with extension_utils.py:89-196, executed the same way:
                    36 cases, the step frame, the channel stack and (square grids) the reset frame.
+  advanced_env.npz AdvancedForestFireBulldozerEnv (advanced_bulldozer.py) built, reset and stepped through
+                   stateless_step (:332-399) the same way: 2 cases (32^2 x 3 envs x 8 steps; 24^2 x 2 envs x 6
+                   steps with extensions), the seeded initial state, each step's actions and every env's draws,
+                   and the whole step's outputs (grid, ages, wind, dousing, clock, position, frame, reward,
+                   terminated, counters).
 
 Usage:  python tests/golden/make_golden.py [fixture ...]   (default: all)
 """
@@ -712,10 +717,106 @@ def gen_pinecones_jax(R, rng):
     return out
 
 
+def _load_advanced_env(js, rlog):
+    """advanced_bulldozer.py with its real operators (ca_alexandridis_jax, move_modify_jax, repeat_ca_jax),
+    extension_utils and init_utils, all loaded under the jax stand-in (`rlog` receives every draw)."""
+    ops = sys.modules["gym_cellular_automata.forest_fire.operators"]
+    r = types.ModuleType("gym_cellular_automata.forest_fire.bulldozer.utils.advanced_bulldozer_render")
+    r.render, r.plot_grid_attribute = (lambda *a, **k: None), (lambda *a, **k: None)
+    sys.modules[r.__name__] = r
+    with js.installed(rlog):
+        aj = _load("gym_cellular_automata.forest_fire.operators.ca_alexandridis_jax",
+                   f"{REF}/forest_fire/operators/ca_alexandridis_jax.py")
+        mmj = _load("gym_cellular_automata.forest_fire.operators.move_modify_jax",
+                    f"{REF}/forest_fire/operators/move_modify_jax.py")
+        rcj = _load("gym_cellular_automata.forest_fire.operators.repeat_ca_jax",
+                    f"{REF}/forest_fire/operators/repeat_ca_jax.py")
+        ops.PartiallyObservableForestFireJax = aj.PartiallyObservableForestFireJax
+        ops.MoveJax, ops.ModifyJax, ops.MoveModifyJax = mmj.MoveJax, mmj.ModifyJax, mmj.MoveModifyJax
+        ops.RepeatCAJax = rcj.RepeatCAJax
+        iu = _load("gym_cellular_automata.forest_fire.bulldozer.utils.init_utils",
+                   f"{REF}/forest_fire/bulldozer/utils/init_utils.py")
+        _load("gym_cellular_automata.forest_fire.bulldozer.utils.extension_utils",
+              f"{REF}/forest_fire/bulldozer/utils/extension_utils.py")
+        ab = _load("gym_cellular_automata.forest_fire.bulldozer.advanced_bulldozer",
+                   f"{REF}/forest_fire/bulldozer/advanced_bulldozer.py")
+    return ab, iu
+
+
+def gen_advanced_env(R, rng):
+    """AdvancedForestFireBulldozerEnv (advanced_bulldozer.py) EXECUTED as published under the jax stand-in: the env
+    built (use_hidden=True: the reference's own init_vegetation / init_density / init_altitude / get_slope /
+    get_winds), reset, a dense mid-episode state written into the reference's own context layout, then consecutive
+    `stateless_step` calls (:332-399: RepeatCAJax -> the Alexandridis rule, MoveModifyJax, time_step / is_night, the
+    RGB observation, reward, terminated, steps_elapsed / reward_accumulated), every env's draws recorded in call order.
+    Pins the batched env step (rows a13-a16, f1) at the env level."""
+    import contextlib
+    import io
+
+    sys.path.insert(0, HERE)
+    import _jax_standin as js
+
+    rlog = js.RandomLog(np.random.default_rng(0))
+    ab, iu = _load_advanced_env(js, rlog)
+    wrap = js.wrap
+    out = {}
+    for ci, (N, E, steps, ext) in enumerate([(32, 3, 8, False), (24, 2, 6, True)]):
+        np.random.seed(4100 + ci)
+        with contextlib.redirect_stdout(io.StringIO()):
+            env = ab.AdvancedForestFireBulldozerEnv(N, N, key=wrap(np.array([7, 0], np.uint32)), num_envs=E,
+                                                    use_hidden=True, enable_extensions=ext)
+            obs, info = env.reset()
+        grid, ctx = obs
+        pe = ctx["per_env_context"]
+        crng = np.random.default_rng(4200 + ci)
+        true_grid = crng.choice([0, 1, 2], size=(E, N, N), p=[0.1, 0.75, 0.15]).astype(np.float32)
+        fire_age = np.where(true_grid == 2, crng.integers(1, 90, (E, N, N)), 0).astype(np.float32)
+        pe["true_grid"] = wrap(true_grid)
+        pe["fire_age"] = wrap(fire_age)
+        pe["dousing_count"] = wrap((crng.random((E, N, N)) < 0.05).astype(np.int32))
+        pe["time_step"] = wrap(np.array([399, 1, 799][:E], np.int32))  # the day / night toggle within the steps
+        ctx["shared_context"]["p_wind_change"] = wrap(np.float32(0.5))
+        pre = f"c{ci}_"
+        out[pre + "meta"] = np.array([N, E, steps, int(ext)])
+        for k in ("vegetation", "density", "altitude", "slope", "wind_index", "is_night", "time_step", "dousing_count",
+                  "true_grid", "fire_age"):
+            out[pre + "init_" + k] = np.asarray(pe[k])
+        out[pre + "init_position"] = np.asarray(ctx["position"])
+        out[pre + "init_time"] = np.asarray(ctx["time"])
+        out[pre + "winds"] = np.asarray(ctx["shared_context"]["winds"])
+        out[pre + "times"] = np.array([env._t_act_move, env._t_act_shoot, env._t_env_any])
+        rlog.gen = np.random.default_rng(4300 + ci)
+        for t in range(steps):
+            n_ext = 3 if ext else 1  # extension choices (0 none, 1 unblur, 2 see-invisible-fires)
+            action = np.stack([crng.integers(0, 9, E), crng.integers(0, 2, E), crng.integers(0, n_ext, E)], axis=1)
+            rlog.log.clear()
+            with contextlib.redirect_stdout(io.StringIO()):
+                obs, reward, term, trunc, info = env.stateless_step(wrap(action.astype(np.int32)), obs, info)
+            rgb, ctx = obs
+            pe = ctx["per_env_context"]
+            kinds = [(k, len(sh)) for k, sh, _, _ in rlog.log]
+            assert kinds == [("uniform", 4), ("uniform", 2), ("randint", 2), ("uniform", 0), ("randint", 0)] * E, kinds
+            st = f"{pre}s{t}_"
+            out[st + "action"] = action
+            for j, name in enumerate(("u_burn", "u_grow", "new_ages", "wind_u", "wind_k")):
+                out[st + name] = np.stack([np.asarray(rlog.log[5 * e + j][2]) for e in range(E)])
+            for k in ("true_grid", "fire_age", "wind_index", "dousing_count", "time_step", "is_night"):
+                out[st + k] = np.asarray(pe[k])
+            out[st + "position"] = np.asarray(ctx["position"])
+            out[st + "time"] = np.asarray(ctx["time"])
+            out[st + "rgb"] = np.asarray(rgb)
+            out[st + "reward"] = np.asarray(reward)
+            out[st + "terminated"] = np.asarray(term)
+            out[st + "steps_elapsed"] = np.asarray(info["steps_elapsed"])
+            out[st + "reward_accumulated"] = np.asarray(info["reward_accumulated"])
+    out["n"] = np.array(2)
+    return out
+
+
 GENERATORS = {"windy": gen_windy, "repeat_ca": gen_repeat, "move_modify": gen_move_modify, "bulldozer": gen_bulldozer,
               "drossel": gen_drossel, "helicopter": gen_helicopter, "moore": gen_moore, "init_utils": gen_init_utils,
               "alexandridis_classic": gen_alexandridis_classic, "alexandridis_jax": gen_alexandridis_jax,
-              "observation": gen_observation, "pinecones_jax": gen_pinecones_jax}
+              "observation": gen_observation, "pinecones_jax": gen_pinecones_jax, "advanced_env": gen_advanced_env}
 
 
 def main():
