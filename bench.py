@@ -33,6 +33,14 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # dousing 1, + slopes: edge layout 4 x f32 = 16 (gca_alex_step_es), 8-plane p_slope 8 x f32 = 32;
 # packed env layout (gca_alex_step_march / _packed): veg|den in one byte, dousing 1 bit, edge slopes 16
 ALEX_BYTES = {"packed": 23.125, "edge": 25, "planes": 41}
+SLOPE_PLANE_BYTES = 16  # 4 edge planes of f32 per cell, not read by the flat-terrain marching step
+
+
+def alex_bytes(env, layout):
+    """Algorithmic bytes per cell-update of the step env.ca_step() launches: the layout's, minus the slope planes when
+    the marching step runs on flat terrain (edge_slope = NULL: 7.125 B)."""
+    flat = getattr(env, "march", False) and getattr(env, "flat_terrain", False)
+    return ALEX_BYTES[layout] - (SLOPE_PLANE_BYTES if flat else 0)
 ALEX_BYTES_PER_CELL = 41  # the SURVEY.md §8d figure (8-plane layout), reported alongside
 WINDY_BYTES_PER_CELL = 2  # u8 read + u8 write
 
@@ -313,12 +321,15 @@ def bench_alex(args, world, rank, device, pg):
     prep = lambda: synthetic_state(env, rank, device)  # every repetition times K steps from the C3 state
     dt, kern = timed_loop(step, args.steps, args.warmup, pg, device, reps=args.reps, detail=detail, prepare=prep)
     cells = world * E * N * N * args.steps
+    nbytes = alex_bytes(env, args.slope_layout)
     res = {
         "value": cells / dt,
         "env_steps_per_s": world * E * args.steps / dt,
         "ms_per_step": dt / args.steps * 1e3,
         "kernel_ms": kern * 1e3,
-        "achieved_gbs": ALEX_BYTES[args.slope_layout] * E * N * N / kern / 1e9,
+        "bytes_per_cell": nbytes,
+        "terrain": "flat" if nbytes != ALEX_BYTES[args.slope_layout] else "general",
+        "achieved_gbs": nbytes * E * N * N / kern / 1e9,
         "survey_equiv_gbs": ALEX_BYTES_PER_CELL * E * N * N / kern / 1e9,
         "fires_left": int((env.counts[:, 2] > 0).sum().item()),
         "timing": detail,
@@ -331,6 +342,20 @@ def bench_alex(args, world, rank, device, pg):
     if getattr(env, "march", False) and rank == 0:
         res["tiled_kernel_ms"] = tiled_kernel_ms(env, device)
     res["pattern_floor_ms"] = march_pattern_ms(env, device)
+    if res["terrain"] == "flat":
+        # the same steps with the slope planes streamed (the step every terrain takes; all factors 1 here): the general
+        # kernel's figures, the headline of rounds 1-6 before the flat-terrain step
+        env.flat_terrain = False
+        dt_g, kern_g = timed_loop(step, args.steps, args.warmup, pg, device, reps=3, prepare=prep)
+        res["general_terrain"] = {
+            "cell_updates_per_s": cells / dt_g, "ms_per_step": dt_g / args.steps * 1e3, "kernel_ms": kern_g * 1e3,
+            "kernel_key": headline_kernel_key(env), "bytes_per_cell": ALEX_BYTES[args.slope_layout],
+            "achieved_gbs": ALEX_BYTES[args.slope_layout] * E * N * N / kern_g / 1e9,
+            "frac": ALEX_BYTES[args.slope_layout] * E * N * N / kern_g / 1e9 / HBM_PEAK_GBS,
+            "pattern_floor_ms": march_pattern_ms(env, device),
+            "note": "gca_alex_step_march reading the env's edge planes (every value 1.0): the step of any terrain "
+                    "(config 4's hidden layers take it)"}
+        env.refresh_terrain()
     if args.headline_only:
         return res
     # the full reference env step: + the RGB observation of stateless_step (advanced_bulldozer.py:1120). The reference's
@@ -494,7 +519,7 @@ def bench_config4(args, world, rank, device, pg):
            "cell_updates_per_s": world * E * N * N * args.steps / dt,
            "env_steps_per_s": world * E * args.steps / dt,
            "kernel_ms": kern * 1e3,
-           "achieved_gbs": ALEX_BYTES[args.slope_layout] * E * N * N / kern / 1e9,
+           "achieved_gbs": alex_bytes(env, args.slope_layout) * E * N * N / kern / 1e9,
            "init_s": init_s,
            "init": "hidden_rng='philox': patches, zero fill, noise, hills and slopes drawn on the device "
                    "(gca_hidden_init, keyed by global env id), altitude arithmetic + get_slope + exp on the device"}
@@ -1058,25 +1083,36 @@ def bench_alex512(args, world, rank, device, pg):
                                          observation="grid")
     env.reset()
     synthetic_state(env, rank, device)
-    times = []
-    for _ in range(3):
-        synthetic_state(env, rank, device)
-        env.ca_step()
-        torch.cuda.synchronize(device)
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record()
-        for _ in range(10):
+
+    def march_kernel_ms():
+        times = []
+        for _ in range(3):
+            synthetic_state(env, rank, device)
             env.ca_step()
-        b.record()
-        torch.cuda.synchronize(device)
-        times.append(a.elapsed_time(b) / 10)
-    march_ms = sorted(times)[1]
+            torch.cuda.synchronize(device)
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            for _ in range(10):
+                env.ca_step()
+            b.record()
+            torch.cuda.synchronize(device)
+            times.append(a.elapsed_time(b) / 10)
+        return sorted(times)[1]
+
+    march_ms, key, nbytes = march_kernel_ms(), headline_kernel_key(env), alex_bytes(env, "packed")
+    general_ms = None
+    if env.flat_terrain:  # the same step reading the slope planes (the step of any terrain)
+        env.flat_terrain = False
+        general_ms = march_kernel_ms()
+        env.refresh_terrain()
     tiled_ms = tiled_kernel_ms(env, device)
     out = {"config": "AdvancedBulldozer 512x512 (R = 7), 1024 envs, use_hidden=False, C3-like mid-episode state",
-           "kernel": headline_kernel_key(env), "march_kernel_ms": march_ms, "tiled_kernel_ms": tiled_ms,
+           "kernel": key, "march_kernel_ms": march_ms, "tiled_kernel_ms": tiled_ms,
            "march_over_tiled": march_ms / tiled_ms,
            "cell_updates_per_s": E * N * N / (march_ms * 1e-3),
-           "moved_gbs": ALEX_BYTES["packed"] * E * N * N / (march_ms * 1e-3) / 1e9}
+           "bytes_per_cell": nbytes,
+           "moved_gbs": nbytes * E * N * N / (march_ms * 1e-3) / 1e9,
+           "general_terrain_march_kernel_ms": general_ms}
     del env
     torch.cuda.empty_cache()
     return out
@@ -1144,7 +1180,8 @@ def headline_kernel_key(env):
     R = int(env.alex_params.R)
     grow = "true" if env.alex_params.p_tree > 0 else "false"
     if getattr(env, "march", False):
-        return f"alex_march<{R}, false, {grow}, {int(env.ncols) // 256}>"
+        flat = "true" if getattr(env, "flat_terrain", False) else "false"
+        return f"alex_march<{R}, false, {grow}, {int(env.ncols) // 256}, {flat}>"
     es = "true" if env.slope_layout in ("packed", "edge") else "false"
     pk = "true" if env.slope_layout == "packed" else "false"
     return f"alex_step<{R}, 0, true, {es}, {pk}, false>"
@@ -1205,7 +1242,8 @@ def copy_bandwidth(device, nbytes=2 << 30, reps=10):
 
 def march_pattern_ms(env, device, frame=False, K=10, reps=3):
     """The headline kernel's access-pattern floor in this run (gca_bench_march_pattern: gca_alex_step_march's loads and
-    stores at W = 256 with trivial arithmetic, on the env's own packed-layout buffers; frame=True adds the fused frame's
+    stores at W = 256 with trivial arithmetic, on the env's own packed-layout buffers, without the slope planes when the
+    env's step runs on flat terrain; frame=True adds the fused frame's
     RGB stores at the frame kernel's 2 waves / SIMD): mean launch time from HIP events, median of `reps`. Scratch
     outputs (the env's state is untouched; the frame buffer is rewritten by the next rendered step). None off the
     marching step."""
@@ -1221,7 +1259,8 @@ def march_pattern_ms(env, device, frame=False, K=10, reps=3):
     go, ao = torch.empty_like(env.grid[a]), torch.empty_like(env.age[a])
     st = dev.stream_ptr(device)
     args = (int(env.alex_params.R), E, H, W, dev.ptr(env.grid[a]), dev.ptr(go), dev.ptr(env.age[a]), dev.ptr(ao),
-            dev.ptr(env.vd), dev.ptr(env.dous_bits), dev.ptr(env.slope_data), dev.ptr(env.rgb if frame else None), st)
+            dev.ptr(env.vd), dev.ptr(env.dous_bits), None if getattr(env, "flat_terrain", False) else dev.ptr(env.slope_data),
+            dev.ptr(env.rgb if frame else None), st)
     times = []
     for _ in range(reps):
         for _ in range(3):
@@ -1314,7 +1353,9 @@ def main():
             "with_rgb_observation": alex.get("with_rgb_observation"),
             "with_rgb_observation_extensions": alex.get("with_rgb_observation_extensions"),
             # achieved = the algorithmic bytes of the step as built (23.125 B per cell-update in the packed layout: every
-            # input byte read once, every output byte written once) x cells / the kernel's mean launch time. SURVEY.md
+            # input byte read once, every output byte written once; 7.125 on flat terrain -- use_hidden=False, this
+            # config -- where the step reads no slope planes and is VALU-bound, see valu_busy and general_terrain)
+            # x cells / the kernel's mean launch time. SURVEY.md
             # §8d's 41 B (the 8-plane layout's bytes) is reported beside it as survey_equiv_*: since the marching
             # kernel it exceeds the 8 TB/s peak (> 1.0), i.e. it no longer measures anything. traffic = PMC bytes.
             "roofline": {"bound": "hbm", "achieved": alex["achieved_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -1322,14 +1363,15 @@ def main():
                          "kernel": alex["kernel"],
                          "kernel_ms": alex["kernel_ms"],
                          "tiled_kernel_ms": alex.get("tiled_kernel_ms"),
-                         "algorithmic_bytes_per_cell": ALEX_BYTES[args.slope_layout],
+                         "algorithmic_bytes_per_cell": alex["bytes_per_cell"],
+                         "terrain": alex["terrain"],
                          "survey_bytes_per_cell": ALEX_BYTES_PER_CELL,
                          "survey_equiv_gbs": alex["survey_equiv_gbs"],
                          "survey_equiv_frac": alex["survey_equiv_gbs"] / HBM_PEAK_GBS,
                          "valu_busy": valu_busy,
                          "profile": prof_info,
                          "slope_layout": args.slope_layout,
-                         "moved_bytes_per_cell": ALEX_BYTES[args.slope_layout],
+                         "moved_bytes_per_cell": alex["bytes_per_cell"],
                          "moved_gbs": alex["achieved_gbs"],
                          "moved_frac": alex["achieved_gbs"] / HBM_PEAK_GBS,
                          "traffic_bytes_per_cell": traffic / (args.envs * args.size * args.size) if traffic else None,
@@ -1342,7 +1384,9 @@ def main():
                          # the same run's floor of the headline kernel's own access pattern (gca_bench_march_pattern)
                          "pattern_floor_ms": alex.get("pattern_floor_ms"),
                          "kernel_over_pattern_floor": (alex["kernel_ms"] / alex["pattern_floor_ms"]
-                                                       if alex.get("pattern_floor_ms") else None)},
+                                                       if alex.get("pattern_floor_ms") else None),
+                         # flat terrain: the same step with the slope planes streamed (rounds 1-6's headline kernel)
+                         "general_terrain": alex.get("general_terrain")},
             "cpu_baseline": cpu,
             "secondary": secondary,
             "config4": config4,

@@ -31,6 +31,9 @@
 
 #include <type_traits>
 
+#ifndef GCA_MARCH_FLAT_OCC
+#define GCA_MARCH_FLAT_OCC 4  // waves / SIMD of the flat-terrain step (no slope planes in registers: ~110 VGPRs)
+#endif
 #ifndef GCA_MARCH_XROW
 #define GCA_MARCH_XROW 1  // the 17th slope row of a tile from the next tile's wave through LDS (r06; 0: from HBM again)
 #endif
@@ -215,11 +218,14 @@ template <class T> __device__ __forceinline__ uint32_t bitcast_u32(T v) { return
 constexpr int XI = 16;
 constexpr int XS_ONE = 13, XS_TWO = 14;  // items holding raw slopes (1.0 in the border slots: factor 1)
 
-template <int R, bool OBS, bool GROW, int NSEG>  // GROW: p_tree > 0 (EMPTY cells draw too); W = 256 * NSEG
+// FLAT: every slope factor is 1 (flat terrain: edge_slope = NULL, e.g. use_hidden=False's init_altitude_same) -- no
+// slope planes are streamed and every row takes the KILL pass (clamp01(base * wind) per direction), bit for bit what
+// the general pass computes with factors of exactly 1.0
+template <int R, bool OBS, bool GROW, int NSEG, bool FLAT>  // GROW: p_tree > 0 (EMPTY cells draw too); W = 256 * NSEG
 // occupancy: 3 waves / SIMD for the step (VGPR-bound, <= 168; 4 would spill), 2 for the fused frame: its 3 KiB per
 // wave-row of f32 RGB stores run faster from fewer concurrent waves (r05g, same box: 1.760 -> 1.723 ms per 4096 x 256^2
 // step with the frame; the plain step at 2 waves: +8 %)
-__global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_waves_per_eu(OBS ? 2 : 3, OBS ? 2 : 3))) void alex_march_kernel(
+__global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_waves_per_eu(OBS ? 2 : (FLAT ? GCA_MARCH_FLAT_OCC : 3), OBS ? 2 : (FLAT ? GCA_MARCH_FLAT_OCC : 3)))) void alex_march_kernel(
     gca_alex_params p, int H, int nwaves, const uint8_t* __restrict__ grid_in, uint8_t* __restrict__ grid_out,
     const int16_t* age_in, int16_t* age_out,  // no __restrict__: the env updates ages in place
     const uint8_t* __restrict__ vd, const uint16_t* __restrict__ dbits, const float* __restrict__ es,
@@ -241,7 +247,7 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
     // cell; 3 of a workgroup's 4 tile boundaries); xok: slot valid. r06 A/B (profiles/r06a, r06b): HBM traffic 24.70 ->
     // 24.15 B / cell; the fused-frame step -1.2 %, but the plain step +0-1.2 % (the one workgroup barrier aligns the
     // four waves' starts) and the reset state's quiet tiles +46 % (0.345 -> 0.503 ms): the plain kernel keeps the 17th row
-    constexpr bool XROW = GCA_MARCH_XROW && !HALO && OBS;
+    constexpr bool XROW = GCA_MARCH_XROW && !HALO && OBS && !FLAT;
     __shared__ float4 xrow[XROW ? 4 : 1][3][XROW ? 64 : 1];
     __shared__ uint32_t xok[XROW ? 4 : 1];
 
@@ -284,7 +290,7 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
     int16_t* aO = age_out + (size_t)e * HW;
     const uint8_t* vE = vd + (size_t)e * HW;
     const uint16_t* dE = dbits + (size_t)e * (HW >> 4);
-    const float* sE = es + (size_t)e * 4 * HW;
+    const float* sE = FLAT ? es : es + (size_t)e * 4 * HW;  // FLAT: es is NULL, never read
     // column of the lane's cell 0 (= its grid byte offset in a row) and its dousing-bit word (u16) in a row
     const uint32_t lc = HALO ? (uint32_t)(MW * g) + 4u * (uint32_t)lane : 4u * (uint32_t)lane;
     const uint32_t ld16 = HALO ? lc >> 4 : (uint32_t)(lane >> 2);
@@ -510,8 +516,12 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
     float4 sc[4], sn[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        sc[k] = ldf4(sE + (size_t)k * HW + (size_t)s0 * W + lc);
-        sn[k] = ldf4(sE + (size_t)k * HW + (size_t)min(s0 + 1, H - 1) * W + lc);
+        if constexpr (FLAT) {
+            sc[k] = sn[k] = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
+        } else {
+            sc[k] = ldf4(sE + (size_t)k * HW + (size_t)s0 * W + lc);
+            sn[k] = ldf4(sE + (size_t)k * HW + (size_t)min(s0 + 1, H - 1) * W + lc);
+        }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -543,8 +553,10 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
         m_edge_own4(v, a, b);
         v = make_float4(col_lo ? 1.0f : a.x, a.y, b.x, col_hi ? 1.0f : b.y);
     };
+    if constexpr (!FLAT) {
 #pragma unroll
-    for (int k = 0; k < 3; ++k) prep_own(sc[k]);
+        for (int k = 0; k < 3; ++k) prep_own(sc[k]);
+    }
 
     // the per-env constants of the packed f32 arithmetic, two per VGPR pair, held in VGPRs: as SGPR operands hipcc
     // materialises every (x, x) pair as two SGPRs, and the 30-odd of them were spilled to VGPR lanes and read back per
@@ -758,10 +770,12 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
             SN[k] = make_float4(col_lo ? 1.0f : oa.x, oa.y, ob.x, col_hi ? 1.0f : ob.y);
         };
         if (!row_need) {
-            load_next_slopes();
-            float unused[4];
+            if constexpr (!FLAT) {
+                load_next_slopes();
+                float unused[4];
 #pragma unroll
-            for (int k = 0; k < 3; ++k) prep_next(k, false, unused);
+                for (int k = 0; k < 3; ++k) prep_next(k, false, unused);
+            }
         } else {
             // ---- heat = heat0 + sum_k dw_k * B_k (k = 0..R, fma chain), minus the dousing term
             gca_f2 ph[2] = {{p.heat0, p.heat0}, {p.heat0, p.heat0}};
@@ -887,10 +901,10 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
                     const float a4[4] = {col_lo ? 1.0f : na.y, nb2.x, nb2.y, nx};
                     apply(4, a4);
                 }
-                load_next_slopes();
+                if constexpr (!FLAT) load_next_slopes();
                 float nb[4];
                 // plane 2 of (r+1, c-1): lane 0's first cell is column 0 (DPP old = 1.0)
-                prep_next(2, !KILL, nb);
+                if constexpr (!FLAT) prep_next(2, !KILL, nb);
                 if (KILL) {
                     apply(5, one);
                 } else {
@@ -900,7 +914,7 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
                     apply(5, a5);
                 }
                 // plane 1 of (r+1, c)
-                prep_next(1, !KILL, nb);
+                if constexpr (!FLAT) prep_next(1, !KILL, nb);
                 if (KILL) {
                     apply(6, one);
                 } else {
@@ -908,7 +922,7 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
                     apply(6, a6);
                 }
                 // plane 0 of (r+1, c+1): lane 63's last cell is column 255 (DPP old = 1.0)
-                prep_next(0, !KILL, nb);
+                if constexpr (!FLAT) prep_next(0, !KILL, nb);
                 if (KILL) {
                     apply(7, one);
                 } else {
@@ -918,7 +932,7 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
                     apply(7, a7);
                 }
             };
-            if (kill_row)
+            if (FLAT || kill_row)
                 dir_pass(std::true_type{});
             else
                 dir_pass(std::false_type{});
@@ -1062,40 +1076,45 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
     }
 }
 
-template <int R, bool OBS, bool GROW, int NSEG>
+template <int R, bool OBS, bool GROW, int NSEG, bool FLAT>
 void launch_march_n(const gca_alex_params& p, int E, int H, const uint8_t* gi, uint8_t* go, const int16_t* ai,
                     int16_t* ao, const uint8_t* vd, const uint16_t* db, const float* es, const int32_t* wi,
                     const uint32_t* rs, int32_t* counts, const uint8_t* act_in, uint8_t* act_out, MarchObs obs,
                     hipStream_t st) {
     const int nwaves = E * (H / SH) * NSEG;
     if constexpr (NSEG == 1)  // four independent tiles per workgroup
-        hipLaunchKernelGGL((alex_march_kernel<R, OBS, GROW, 1>), dim3((unsigned)((nwaves + 3) / 4)), dim3(256), 0, st, p,
+        hipLaunchKernelGGL((alex_march_kernel<R, OBS, GROW, 1, FLAT>), dim3((unsigned)((nwaves + 3) / 4)), dim3(256), 0, st, p,
                            H, nwaves, gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs);
     else  // one strip (NSEG segment waves) per workgroup
-        hipLaunchKernelGGL((alex_march_kernel<R, OBS, GROW, NSEG>), dim3((unsigned)(nwaves / NSEG)), dim3(64 * NSEG), 0,
+        hipLaunchKernelGGL((alex_march_kernel<R, OBS, GROW, NSEG, FLAT>), dim3((unsigned)(nwaves / NSEG)), dim3(64 * NSEG), 0,
                            st, p, H, nwaves, gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs);
 }
-template <int R, bool OBS, bool GROW>
+template <int R, bool OBS, bool GROW, bool FLAT>
 void launch_march_g(const gca_alex_params& p, int E, int H, int W, const uint8_t* gi, uint8_t* go, const int16_t* ai,
                     int16_t* ao, const uint8_t* vd, const uint16_t* db, const float* es, const int32_t* wi,
                     const uint32_t* rs, int32_t* counts, const uint8_t* act_in, uint8_t* act_out, MarchObs obs,
                     hipStream_t st) {
     if (W == MW)
-        launch_march_n<R, OBS, GROW, 1>(p, E, H, gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs, st);
+        launch_march_n<R, OBS, GROW, 1, FLAT>(p, E, H, gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs, st);
     else if (W == 2 * MW)
-        launch_march_n<R, OBS, GROW, 2>(p, E, H, gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs, st);
+        launch_march_n<R, OBS, GROW, 2, FLAT>(p, E, H, gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs, st);
     else
-        launch_march_n<R, OBS, GROW, 4>(p, E, H, gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs, st);
+        launch_march_n<R, OBS, GROW, 4, FLAT>(p, E, H, gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs, st);
 }
 template <int R, bool OBS>
 void launch_march(const gca_alex_params& p, int E, int H, int W, const uint8_t* gi, uint8_t* go, const int16_t* ai,
                   int16_t* ao, const uint8_t* vd, const uint16_t* db, const float* es, const int32_t* wi,
                   const uint32_t* rs, int32_t* counts, const uint8_t* act_in, uint8_t* act_out, MarchObs obs,
                   hipStream_t st) {
-    if (p.p_tree > 0.0f)
-        launch_march_g<R, OBS, true>(p, E, H, W, gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs, st);
+    const bool grow = p.p_tree > 0.0f;
+    if (es && grow)
+        launch_march_g<R, OBS, true, false>(p, E, H, W, gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs, st);
+    else if (es)
+        launch_march_g<R, OBS, false, false>(p, E, H, W, gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs, st);
+    else if (grow)
+        launch_march_g<R, OBS, true, true>(p, E, H, W, gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs, st);
     else
-        launch_march_g<R, OBS, false>(p, E, H, W, gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs, st);
+        launch_march_g<R, OBS, false, true>(p, E, H, W, gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs, st);
 }
 
 template <bool OBS>
@@ -1116,8 +1135,8 @@ int march_impl(const gca_alex_params* p, int E, int H, int W, const uint8_t* gri
                const int16_t* age_in, int16_t* age_out, const uint8_t* vd, const uint16_t* dous_bits,
                const float* edge_slope, const int32_t* wind_index, const uint32_t* rng_step, int32_t* counts,
                const uint8_t* act_in, uint8_t* act_out, MarchObs obs, void* stream) {
-    GCA_CHECK_ARG(p && grid_in && grid_out && age_in && age_out && vd && dous_bits && edge_slope && wind_index,
-                  "alex_step_march: null argument");
+    GCA_CHECK_ARG(p && grid_in && grid_out && age_in && age_out && vd && dous_bits && wind_index,
+                  "alex_step_march: null argument");  // edge_slope NULL: flat terrain (every slope factor 1)
     GCA_CHECK_ARG(E > 0 && H > 0 && (W == MW || W == 2 * MW || W == 4 * MW) && H % SH == 0,
                   "alex_step_march: W must be 256, 512 or 1024 and H a multiple of 16");
     GCA_CHECK_ARG(p->R >= 1 && p->R <= GCA_MAX_RADIUS, "alex_step_march: burn radius must be in [1, 8]");

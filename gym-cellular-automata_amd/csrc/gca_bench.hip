@@ -11,7 +11,8 @@
 //                             stores, and with `rgb` the fused frame's three 1-KiB f32 stores per wave-row. It reads
 //                             and writes the same 23.125 B / cell (+ 12 written with the frame) as the step, so its
 //                             time is the floor of that pattern on this device: kernel_ms / pattern_ms says how far the
-//                             step's instruction stream sits above it.
+//                             step's instruction stream sits above it. edge_slopes = NULL: the flat-terrain step's
+//                             pattern (no slope planes: 7.125 B / cell, 4 waves / SIMD as that step).
 #include "gca_common.h"
 
 typedef float gvf4 __attribute__((ext_vector_type(4)));
@@ -43,8 +44,8 @@ extern "C" int gca_bench_copy(const void* src, void* dst, int64_t nbytes, int nt
     return GCA_OK;
 }
 
-template <int R, bool FRAME>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FRAME ? 2 : 3, FRAME ? 2 : 3))) void
+template <int R, bool FRAME, bool FLAT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FRAME ? 2 : (FLAT ? 4 : 3), FRAME ? 2 : (FLAT ? 4 : 3)))) void
 bench_march_pattern_kernel(int H, int nwaves, const uint8_t* __restrict__ g, uint8_t* __restrict__ go,
                            const int16_t* __restrict__ a, int16_t* __restrict__ ao, const uint8_t* __restrict__ vd,
                            const uint16_t* __restrict__ db, const float* __restrict__ es, gvf4* __restrict__ rgb) {
@@ -58,7 +59,7 @@ bench_march_pattern_kernel(int H, int nwaves, const uint8_t* __restrict__ g, uin
     const int strips = H / SH, e = wv / strips, s0 = (wv - e * strips) * SH;
     const uint32_t HW = (uint32_t)H * W;
     const uint8_t* gE = g + (size_t)e * HW;
-    const gvf4* sE = reinterpret_cast<const gvf4*>(es + (size_t)e * 4 * HW);
+    const gvf4* sE = reinterpret_cast<const gvf4*>(FLAT ? es : es + (size_t)e * 4 * HW);
     const uint8_t* vE = vd + (size_t)e * HW;
     const int16_t* aE = a + (size_t)e * HW;
     const uint16_t* dE = db + (size_t)e * (HW >> 4);
@@ -73,7 +74,9 @@ bench_march_pattern_kernel(int H, int nwaves, const uint8_t* __restrict__ g, uin
     gvu2 ag[2];
     auto slopes = [&](int rs, gvf4(&o)[4]) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) o[k] = __builtin_nontemporal_load(&sE[(k * HW + (uint32_t)rs * W) / 4 + lane]);
+        for (int k = 0; k < 4; ++k)
+            o[k] = FLAT ? (gvf4){1.0f, 1.0f, 1.0f, 1.0f}
+                        : __builtin_nontemporal_load(&sE[(k * HW + (uint32_t)rs * W) / 4 + lane]);
     };
     auto issue = [&](int i, int sl_slot) {
         const int r = s0 + i;
@@ -120,23 +123,31 @@ bench_march_pattern_kernel(int H, int nwaves, const uint8_t* __restrict__ g, uin
     }
 }
 
-template <int R>
-static void launch_pattern(int E, int H, const uint8_t* g, uint8_t* go, const int16_t* a, int16_t* ao,
-                           const uint8_t* vd, const uint16_t* db, const float* es, float* rgb, hipStream_t st) {
+template <int R, bool FLAT>
+static void launch_pattern_f(int E, int H, const uint8_t* g, uint8_t* go, const int16_t* a, int16_t* ao,
+                             const uint8_t* vd, const uint16_t* db, const float* es, float* rgb, hipStream_t st) {
     const int nwaves = E * (H / 16);
     const dim3 grid((unsigned)((nwaves + 3) / 4));
     if (rgb)
-        hipLaunchKernelGGL((bench_march_pattern_kernel<R, true>), grid, dim3(256), 0, st, H, nwaves, g, go, a, ao, vd, db,
-                           es, (gvf4*)rgb);
+        hipLaunchKernelGGL((bench_march_pattern_kernel<R, true, FLAT>), grid, dim3(256), 0, st, H, nwaves, g, go, a, ao,
+                           vd, db, es, (gvf4*)rgb);
     else
-        hipLaunchKernelGGL((bench_march_pattern_kernel<R, false>), grid, dim3(256), 0, st, H, nwaves, g, go, a, ao, vd,
-                           db, es, (gvf4*)nullptr);
+        hipLaunchKernelGGL((bench_march_pattern_kernel<R, false, FLAT>), grid, dim3(256), 0, st, H, nwaves, g, go, a,
+                           ao, vd, db, es, (gvf4*)nullptr);
+}
+template <int R>
+static void launch_pattern(int E, int H, const uint8_t* g, uint8_t* go, const int16_t* a, int16_t* ao,
+                           const uint8_t* vd, const uint16_t* db, const float* es, float* rgb, hipStream_t st) {
+    if (es)
+        launch_pattern_f<R, false>(E, H, g, go, a, ao, vd, db, es, rgb, st);
+    else
+        launch_pattern_f<R, true>(E, H, g, go, a, ao, vd, db, es, rgb, st);
 }
 
 extern "C" int gca_bench_march_pattern(int R, int E, int H, int W, const uint8_t* grid, uint8_t* grid_out,
                                        const int16_t* age, int16_t* age_out, const uint8_t* vd,
                                        const uint16_t* dous_bits, const float* edge_slopes, float* rgb, void* stream) {
-    GCA_CHECK_ARG(grid && grid_out && age && age_out && vd && dous_bits && edge_slopes, "buffers required");
+    GCA_CHECK_ARG(grid && grid_out && age && age_out && vd && dous_bits, "buffers required");
     GCA_CHECK_ARG(W == 256, "the pattern of the W = 256 marching step only");
     GCA_CHECK_ARG(E >= 1 && H >= 16 && H % 16 == 0, "E >= 1, H a multiple of 16");
     GCA_CHECK_ARG((int64_t)E * H * W < (int64_t)1 << 31, "E * H * W must stay below 2^31");

@@ -255,6 +255,15 @@ class AdvancedForestFireBulldozerEnv:
             del tmp
         else:
             call("gca_alex_slope_from_altitude", dev.ptr(altitude), dev.ptr(self.slope_data), None, E, H, W, st)
+        self.refresh_terrain()
+
+    def refresh_terrain(self):
+        """Re-derive `flat_terrain` from the slope buffer: True when every edge value is +-1, i.e. every slope factor of
+        every env is exactly 1 (use_hidden=False: init_altitude_same gives zero slopes, exp_f32(0) = 1). The marching
+        step then streams no slope planes (gca_alex_step_march with edge_slope = NULL; bit for bit the same step).
+        The env calls it whenever it sets the slopes (construction, set_state(altitude=...), adopted contexts); call it
+        after writing `slope_data` in place."""
+        self.flat_terrain = self.slope_layout != "planes" and bool((self.slope_data.abs() == 1.0).all())
 
     def p_slope_planes(self):
         """The general 8-plane p_slope (E, 8, H, W) = exp_f32(0.078 * slope) of this env's altitude
@@ -559,12 +568,14 @@ class AdvancedForestFireBulldozerEnv:
 
         if kind == "env":
             self.slope_data.copy_(t)
+            self.refresh_terrain()
             return
         # arbitrary slopes need the general layout: 8 p_slope planes (gca_alex_step, 41 B per cell-update)
         if self.slope_layout != "planes":
             self._to_planes_layout()
         E, H, W = self.num_envs, self.nrows, self.ncols
         call("gca_alex_prepare_slope", dev.ptr(t), dev.ptr(self.slope_data), E, H, W, dev.stream_ptr(self.device))
+        self.refresh_terrain()
 
     def _to_planes_layout(self):
         """Switch the step to the 8-plane p_slope layout (gca_alex_step) keeping the state: separate age buffers,
@@ -674,7 +685,8 @@ class AdvancedForestFireBulldozerEnv:
         if self.slope_layout == "packed":
             args = (self.alex_params, E, H, W, dev.ptr(self.grid[a]), dev.ptr(self.grid[b]),
                     dev.ptr(self.age[a]), dev.ptr(self.age[b]), dev.ptr(self.vd), dev.ptr(self.dous_bits),
-                    dev.ptr(self.slope_data), dev.ptr(self.wind_index), dev.ptr(self.rng_step), dev.ptr(self.counts),
+                    dev.ptr(None if self.march and self.flat_terrain else self.slope_data), dev.ptr(self.wind_index),
+                    dev.ptr(self.rng_step), dev.ptr(self.counts),
                     dev.ptr(None if self.act is None else self.act[a]), dev.ptr(None if self.act is None else self.act[b]))
             fn = "gca_alex_step_march" if self.march else "gca_alex_step_packed"
             if render:

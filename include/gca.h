@@ -237,7 +237,9 @@ int gca_alex_step_packed_rgb(const gca_alex_params* p, int E, int H, int W, cons
 /* gca_alex_step_packed / _rgb in marching form for W == 256 (H % 16 == 0): one wave walks one 16 x 256 tile row by
  * row (gca_alex_march.hip), every slope byte read once. Same replaced code, arguments, results (bit for bit), tile
  * activity map and frame, except edge_slope: the edge layout (E,4,H,W) in natural column order (the output of
- * gca_alex_edge_slope_from_altitude, not coalesced). */
+ * gca_alex_edge_slope_from_altitude, not coalesced), or NULL for flat terrain: every slope factor 1, as when every edge
+ * value is +-1 (use_hidden=False: init_altitude_same, advanced_bulldozer.py:190-197, gives zero slopes) — no slope
+ * planes are read (7.125 instead of 23.125 B / cell) and the results are those of the all-ones planes, bit for bit. */
 int gca_alex_step_march(const gca_alex_params* p, int E, int H, int W, const uint8_t* grid_in, uint8_t* grid_out,
                         const int16_t* age_in, int16_t* age_out, const uint8_t* vd, const uint16_t* dous_bits,
                         const float* edge_slope, const int32_t* wind_index, const uint32_t* rng_step, int32_t* counts,
@@ -483,7 +485,8 @@ int gca_ds_step(const uint8_t* grid_in, uint8_t* grid_out, int E, int H, int W, 
  * loads and stores: the practical HBM ceiling the bench reports beside the 8 TB/s spec.
  * gca_bench_march_pattern: the loads and stores of gca_alex_step_march at W = 256 (radius R in 4..7; with rgb != NULL
  * also the fused frame's f32 RGB stores) with trivial arithmetic, on the env's packed-layout buffers: the floor of
- * that access pattern on this device. Outputs are scratch (their values mean nothing). */
+ * that access pattern on this device; edge_slopes = NULL: the flat-terrain step's pattern (no slope planes). Outputs are
+ * scratch (their values mean nothing). */
 int gca_bench_copy(const void* src, void* dst, int64_t nbytes, int nt, void* stream);
 int gca_bench_march_pattern(int R, int E, int H, int W, const uint8_t* grid, uint8_t* grid_out, const int16_t* age,
                             int16_t* age_out, const uint8_t* vd, const uint16_t* dous_bits, const float* edge_slopes,

@@ -353,3 +353,75 @@ def test_env_march_equals_tiled_at_wide_grids(device, N, pinecones):
             for env in envs:
                 env.done[0] = 1
                 env.conditional_reset()
+
+
+@pytest.mark.parametrize("R,W,p_tree,seed", [(6, 256, 0.0, 81), (1, 256, 0.01, 82), (8, 256, 0.0, 83), (7, 512, 0.0, 84),
+                                             (3, 512, 0.01, 85), (6, 1024, 0.0, 86)])
+def test_flat_terrain_step_equals_unit_planes(device, R, W, p_tree, seed):
+    """edge_slope = NULL (the flat-terrain instance: no slope planes read, every row through the factor-free pass) equals
+    the general step on all-ones edge planes, bit for bit: grid, ages, counts and tile map over three chained steps,
+    the fused frame at W = 256 (day and night), with and without the tile activity map."""
+    import torch
+
+    from gymca_amd import _device as dev
+    from gymca_amd._lib import call
+    from gymca_amd.forest_fire.bulldozer.observation import make_obs_params
+
+    E, H = 3, 48
+    case = make_case(E, H, W, seed, p_tree=p_tree, dousing_p=0.2, fire_p=0.05)
+    p = _with_radius(params(H, p_tree, seed=seed * 3), R)
+    ones = torch.ones((E, 4, H, W), dtype=torch.float32, device=device)
+    vd, bits = _layers(device, case)
+    rgb = None
+    if W == 256:
+        col = torch.zeros((12, 4), dtype=torch.float32, device=device)
+        call("gca_obs_color_table", make_obs_params(0, 1, 2, False, False, 8), dev.ptr(col), dev.stream_ptr())
+        rgb = (col, torch.as_tensor(np.arange(E, dtype=np.int32) % 2, device=device))
+    for s in range(3):
+        rs = np.full(E, 11 * s + 1, np.uint32)
+        for fn, extra in (("gca_alex_step_march", {}),) + ((("gca_alex_step_march_rgb", {"rgb": rgb}),) if rgb else ()):
+            act = np.ones((E, H // 16), np.uint8) if (W == 256 and p_tree == 0.0) else None
+            ref = _run(device, fn, p, case, ones, rs, vd, bits, act_in=act, **extra)
+            got = _run(device, fn, p, case, None, rs, vd, bits, act_in=act, **extra)
+            for k in range(5):
+                if ref[k] is not None:
+                    assert np.array_equal(got[k], ref[k]), (fn, s, k)
+        case["grid"], case["age"] = ref[0], ref[1]
+        assert (ref[0] == 2).any()
+
+
+@pytest.mark.parametrize("extensions", [False, True])
+def test_env_flat_terrain_equals_general(device, extensions):
+    """use_hidden=False gives flat terrain: the env's step takes edge_slope = NULL (env.flat_terrain) and equals, bit for
+    bit, the same env forced through the general step (slope planes read): grid, ages, counts, reward and the fused
+    RGB frame (plain, or the extension pipeline with the three choices mixed), over steps with a conditional reset;
+    a non-flat slope buffer written in place is picked up by refresh_terrain()."""
+    import torch
+
+    from gymca_amd.forest_fire.bulldozer import AdvancedForestFireBulldozerEnv
+
+    E, N = 6, 256
+    envs = [AdvancedForestFireBulldozerEnv(N, N, key=5, num_envs=E, use_hidden=False, device=device, observation="rgb",
+                                           enable_extensions=extensions) for _ in range(2)]
+    assert all(env.flat_terrain for env in envs)
+    envs[1].flat_terrain = False
+    for env in envs:
+        env.reset()
+        env.pos[:, 0], env.pos[:, 1] = 190, 60
+    rng = np.random.default_rng(3)
+    for s in range(6):
+        act = np.stack([rng.integers(0, 9, E), rng.integers(0, 2, E), rng.integers(0, 3, E)], axis=1).astype(np.int32)
+        outs = [env.step(torch.as_tensor(act, device=device)) for env in envs]
+        a, b = envs
+        assert torch.equal(a.grid[a.cur], b.grid[b.cur]) and torch.equal(a.age[a.cur], b.age[b.cur]), s
+        assert torch.equal(a.counts, b.counts) and torch.equal(outs[0][1], outs[1][1]), s
+        assert torch.equal(a.rgb, b.rgb), s
+        if s == 3:
+            for env in envs:
+                env.done[1] = 1
+                env.conditional_reset()
+    assert int(envs[0].counts[:, 2].sum()) > 0
+    env = envs[0]
+    env.slope_data[:, 0, 5, 5] = 1.5
+    env.refresh_terrain()
+    assert not env.flat_terrain
