@@ -850,13 +850,19 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
                     const uint32_t Md = dir_mask(d);
                     // the two cell pairs' chains interleaved step by step (a packed f32 result read by the next
                     // instruction costs a wait state; two independent chains hide it)
-                    gca_f2 t[2], c[2];
+                    // (KILL: every factor 1, so clamp01(base * wind) is the product's own clamp modifier -- one packed
+                    //  op per pair; with the flat-terrain step every row takes it)
+                    gca_f2 c[2];
+                    if constexpr (KILL) {
 #pragma unroll
-                    for (int h = 0; h < 2; ++h) t[h] = ph[h] * wd2;
+                        for (int h = 0; h < 2; ++h) c[h] = gca_pk_mul_clamp01(ph[h], wd2);
+                    } else {
+                        gca_f2 t[2];
 #pragma unroll
-                    for (int h = 0; h < 2; ++h)
-                        c[h] = KILL ? (gca_f2){gca_clamp01(t[h].x), gca_clamp01(t[h].y)}
-                                    : gca_pk_mul_clamp01(t[h], (gca_f2){a[2 * h], a[2 * h + 1]});
+                        for (int h = 0; h < 2; ++h) t[h] = ph[h] * wd2;
+#pragma unroll
+                        for (int h = 0; h < 2; ++h) c[h] = gca_pk_mul_clamp01(t[h], (gca_f2){a[2 * h], a[2 * h + 1]});
+                    }
                     // qn <- fma(-qn, c, qn) = qn * (1 - c), one rounding (the oracle's order); no burning
                     // neighbour d: c -> +0 and qn is unchanged exactly (the oracle skips the factor)
                     uint32_t cm[2][2];
@@ -1125,8 +1131,12 @@ void dispatch_march(const gca_alex_params& p, int E, int H, int W, const uint8_t
 #define GCA_MARCH_CASE(RV) \
     case RV: launch_march<RV, OBS>(p, E, H, W, gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs, st); break;
     switch (p.R) {
+#ifdef GCA_MARCH_ANALYSIS_R6  // ISA analysis builds (scripts/isa_rows.py): the R = 6 instances only
+        GCA_MARCH_CASE(6)
+#else
         GCA_MARCH_CASE(1) GCA_MARCH_CASE(2) GCA_MARCH_CASE(3) GCA_MARCH_CASE(4)
         GCA_MARCH_CASE(5) GCA_MARCH_CASE(6) GCA_MARCH_CASE(7) GCA_MARCH_CASE(8)
+#endif
     }
 #undef GCA_MARCH_CASE
 }
