@@ -34,13 +34,16 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # packed env layout (gca_alex_step_march / _packed): veg|den in one byte, dousing 1 bit, edge slopes 16
 ALEX_BYTES = {"packed": 23.125, "edge": 25, "planes": 41}
 SLOPE_PLANE_BYTES = 16  # 4 edge planes of f32 per cell, not read by the flat-terrain marching step
+VD_BYTES = 1  # the packed vegetation / density byte, not read by the uniform-layers step
 
 
 def alex_bytes(env, layout):
     """Algorithmic bytes per cell-update of the step env.ca_step() launches: the layout's, minus the slope planes when
-    the marching step runs on flat terrain (edge_slope = NULL: 7.125 B)."""
+    the marching step runs on flat terrain (edge_slope = NULL: 7.125 B) and the vd layer when the layers are uniform
+    too (vd = NULL: 6.125 B)."""
     flat = getattr(env, "march", False) and getattr(env, "flat_terrain", False)
-    return ALEX_BYTES[layout] - (SLOPE_PLANE_BYTES if flat else 0)
+    uni = flat and getattr(env, "uniform_layers", False)
+    return ALEX_BYTES[layout] - (SLOPE_PLANE_BYTES if flat else 0) - (VD_BYTES if uni else 0)
 ALEX_BYTES_PER_CELL = 41  # the SURVEY.md §8d figure (8-plane layout), reported alongside
 WINDY_BYTES_PER_CELL = 2  # u8 read + u8 write
 
@@ -328,7 +331,8 @@ def bench_alex(args, world, rank, device, pg):
         "ms_per_step": dt / args.steps * 1e3,
         "kernel_ms": kern * 1e3,
         "bytes_per_cell": nbytes,
-        "terrain": "flat" if nbytes != ALEX_BYTES[args.slope_layout] else "general",
+        "terrain": ("general" if nbytes == ALEX_BYTES[args.slope_layout] else
+                    "flat, uniform layers" if getattr(env, "uniform_layers", False) else "flat"),
         "achieved_gbs": nbytes * E * N * N / kern / 1e9,
         "survey_equiv_gbs": ALEX_BYTES_PER_CELL * E * N * N / kern / 1e9,
         "fires_left": int((env.counts[:, 2] > 0).sum().item()),
@@ -342,7 +346,7 @@ def bench_alex(args, world, rank, device, pg):
     if getattr(env, "march", False) and rank == 0:
         res["tiled_kernel_ms"] = tiled_kernel_ms(env, device)
     res["pattern_floor_ms"] = march_pattern_ms(env, device)
-    if res["terrain"] == "flat":
+    if res["terrain"] != "general":
         # the same steps with the slope planes streamed (the step every terrain takes; all factors 1 here): the general
         # kernel's figures, the headline of rounds 1-6 before the flat-terrain step
         env.flat_terrain = False
@@ -1180,8 +1184,9 @@ def headline_kernel_key(env):
     R = int(env.alex_params.R)
     grow = "true" if env.alex_params.p_tree > 0 else "false"
     if getattr(env, "march", False):
-        flat = "true" if getattr(env, "flat_terrain", False) else "false"
-        return f"alex_march<{R}, false, {grow}, {int(env.ncols) // 256}, {flat}>"
+        flat = getattr(env, "flat_terrain", False)
+        fm = 0 if not flat else (2 if getattr(env, "uniform_layers", False) else 1)
+        return f"alex_march<{R}, false, {grow}, {int(env.ncols) // 256}, {fm}>"
     es = "true" if env.slope_layout in ("packed", "edge") else "false"
     pk = "true" if env.slope_layout == "packed" else "false"
     return f"alex_step<{R}, 0, true, {es}, {pk}, false>"
@@ -1256,10 +1261,12 @@ def march_pattern_ms(env, device, frame=False, K=10, reps=3):
         return None
     E, H, W = env.num_envs, env.nrows, env.ncols
     a = env.cur
+    flat = getattr(env, "flat_terrain", False)
     go, ao = torch.empty_like(env.grid[a]), torch.empty_like(env.age[a])
     st = dev.stream_ptr(device)
     args = (int(env.alex_params.R), E, H, W, dev.ptr(env.grid[a]), dev.ptr(go), dev.ptr(env.age[a]), dev.ptr(ao),
-            dev.ptr(env.vd), dev.ptr(env.dous_bits), None if getattr(env, "flat_terrain", False) else dev.ptr(env.slope_data),
+            None if flat and getattr(env, "uniform_layers", False) else dev.ptr(env.vd), dev.ptr(env.dous_bits),
+            None if flat else dev.ptr(env.slope_data),
             dev.ptr(env.rgb if frame else None), st)
     times = []
     for _ in range(reps):
@@ -1354,7 +1361,8 @@ def main():
             "with_rgb_observation_extensions": alex.get("with_rgb_observation_extensions"),
             # achieved = the algorithmic bytes of the step as built (23.125 B per cell-update in the packed layout: every
             # input byte read once, every output byte written once; 7.125 on flat terrain -- use_hidden=False, this
-            # config -- where the step reads no slope planes and is VALU-bound, see valu_busy and general_terrain)
+            # config -- where the step reads no slope planes, and 6.125 with its uniform layers, where it reads no vd
+            # layer either; that step is VALU-bound, see valu_busy and general_terrain)
             # x cells / the kernel's mean launch time. SURVEY.md
             # §8d's 41 B (the 8-plane layout's bytes) is reported beside it as survey_equiv_*: since the marching
             # kernel it exceeds the 8 TB/s peak (> 1.0), i.e. it no longer measures anything. traffic = PMC bytes.

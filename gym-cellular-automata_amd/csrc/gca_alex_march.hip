@@ -218,14 +218,16 @@ template <class T> __device__ __forceinline__ uint32_t bitcast_u32(T v) { return
 constexpr int XI = 16;
 constexpr int XS_ONE = 13, XS_TWO = 14;  // items holding raw slopes (1.0 in the border slots: factor 1)
 
-// FLAT: every slope factor is 1 (flat terrain: edge_slope = NULL, e.g. use_hidden=False's init_altitude_same) -- no
-// slope planes are streamed and every row takes the KILL pass (clamp01(base * wind) per direction), bit for bit what
-// the general pass computes with factors of exactly 1.0
-template <int R, bool OBS, bool GROW, int NSEG, bool FLAT>  // GROW: p_tree > 0 (EMPTY cells draw too); W = 256 * NSEG
+// FLATM 1 / 2 (FLAT): every slope factor is 1 (flat terrain: edge_slope = NULL, e.g. use_hidden=False's
+// init_altitude_same) -- no slope planes are streamed and every row takes the KILL pass (clamp01(base * wind) per
+// direction), bit for bit what the general pass computes with factors of exactly 1.0. FLATM 2 (UNI): also every cell's
+// vegetation / density byte is p.vd_uniform (vd = NULL; use_hidden=False's init_vegetation_same / init_density_same):
+// the vd stream and the per-cell LUT reads go, the two factors are wave constants (the same f32 products in order)
+template <int R, bool OBS, bool GROW, int NSEG, int FLATM>  // GROW: p_tree > 0 (EMPTY cells draw too); W = 256 * NSEG
 // occupancy: 3 waves / SIMD for the step (VGPR-bound, <= 168; 4 would spill), 2 for the fused frame: its 3 KiB per
 // wave-row of f32 RGB stores run faster from fewer concurrent waves (r05g, same box: 1.760 -> 1.723 ms per 4096 x 256^2
 // step with the frame; the plain step at 2 waves: +8 %)
-__global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_waves_per_eu(OBS ? 2 : (FLAT ? GCA_MARCH_FLAT_OCC : 3), OBS ? 2 : (FLAT ? GCA_MARCH_FLAT_OCC : 3)))) void alex_march_kernel(
+__global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_waves_per_eu(OBS ? 2 : (FLATM ? GCA_MARCH_FLAT_OCC : 3), OBS ? 2 : (FLATM ? GCA_MARCH_FLAT_OCC : 3)))) void alex_march_kernel(
     gca_alex_params p, int H, int nwaves, const uint8_t* __restrict__ grid_in, uint8_t* __restrict__ grid_out,
     const int16_t* age_in, int16_t* age_out,  // no __restrict__: the env updates ages in place
     const uint8_t* __restrict__ vd, const uint16_t* __restrict__ dbits, const float* __restrict__ es,
@@ -247,6 +249,7 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
     // cell; 3 of a workgroup's 4 tile boundaries); xok: slot valid. r06 A/B (profiles/r06a, r06b): HBM traffic 24.70 ->
     // 24.15 B / cell; the fused-frame step -1.2 %, but the plain step +0-1.2 % (the one workgroup barrier aligns the
     // four waves' starts) and the reset state's quiet tiles +46 % (0.345 -> 0.503 ms): the plain kernel keeps the 17th row
+    constexpr bool FLAT = FLATM >= 1, UNI = FLATM == 2;
     constexpr bool XROW = GCA_MARCH_XROW && !HALO && OBS && !FLAT;
     __shared__ float4 xrow[XROW ? 4 : 1][3][XROW ? 64 : 1];
     __shared__ uint32_t xok[XROW ? 4 : 1];
@@ -288,7 +291,7 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
     uint8_t* gO = grid_out + (size_t)e * HW;
     const int16_t* aE = age_in + (size_t)e * HW;
     int16_t* aO = age_out + (size_t)e * HW;
-    const uint8_t* vE = vd + (size_t)e * HW;
+    const uint8_t* vE = UNI ? vd : vd + (size_t)e * HW;  // UNI: vd is NULL, never read
     const uint16_t* dE = dbits + (size_t)e * (HW >> 4);
     const float* sE = FLAT ? es : es + (size_t)e * 4 * HW;  // FLAT: es is NULL, never read
     // column of the lane's cell 0 (= its grid byte offset in a row) and its dousing-bit word (u16) in a row
@@ -511,7 +514,7 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
     // row r's own codes are re-read one row ahead (nOwn) although the ring saw them R rows earlier: a per-wave LDS ring
     // of the codes instead cuts the traffic by 1.0 B / cell (26.2 -> 25.2) but measured 0.6-2 % slower (r03q/r03r)
     uint32_t nG = graw(s0 + R), nD = draw_bits(s0 + 2), nOwn = graw(s0);
-    uint32_t nVD = *reinterpret_cast<const uint32_t*>(vE + (size_t)s0 * W + lc);
+    uint32_t nVD = UNI ? 0u : *reinterpret_cast<const uint32_t*>(vE + (size_t)s0 * W + lc);
     uint2 nAge = *reinterpret_cast<const uint2*>(aE + (size_t)s0 * W + lc);
     float4 sc[4], sn[4];
 #pragma unroll
@@ -579,6 +582,13 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
             asm volatile("" : "+v"(hdwp[q]));
         }
     }
+    // UNI: the two layer factors (1 + p_veg, 1 + p_den) of every cell, as the LUT entries of the uniform vd byte
+    gca_f2 avd = {1.0f, 1.0f};
+    if constexpr (UNI) {
+        const int b = p.vd_uniform & 0xFF;
+        avd = (gca_f2){gca_alex_lut_entry(p, b & 7), gca_alex_lut_entry(p, 8 + ((b >> 4) & 7))};
+        asm volatile("" : "+v"(avd));
+    }
     auto bcast = [](gca_f2 v, int h) -> gca_f2 {
         return h ? __builtin_shufflevector(v, v, 1, 1) : __builtin_shufflevector(v, v, 0, 0);
     };
@@ -638,7 +648,7 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
             const uint32_t gl = ld_at<uint32_t>(gE + (size_t)min(rg, H - 1) * W, lc);
             const uint32_t d = ld_at<uint16_t>(dE + (size_t)min(rd, H - 1) * (W / 16), lane_d);
             nOwn = ld_at<uint32_t>(gE + (size_t)r1 * W, lc);
-            nVD = ld_nt<uint32_t>(vE + (size_t)r1 * W, lc);
+            if constexpr (!UNI) nVD = ld_nt<uint32_t>(vE + (size_t)r1 * W, lc);
             nAge = ld_nt<uint2>(aE + (size_t)r1 * W, lane_a);
             nG = rg < H ? gl : Ep;
             nD = rd < H ? d : 0u;
@@ -824,7 +834,12 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
                 for (int h = 0; h < 2; ++h) ph[h] = ph[h] - dz[h];
             }
             // ---- base = (p_h * (1 + p_veg)) * (1 + p_den)
-            {
+            if constexpr (UNI) {
+#pragma unroll
+                for (int h = 0; h < 2; ++h) ph[h] = ph[h] * bcast(avd, 0);
+#pragma unroll
+                for (int h = 0; h < 2; ++h) ph[h] = ph[h] * bcast(avd, 1);
+            } else {
                 gca_f2 av[2], ad[2];
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
@@ -1082,45 +1097,52 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
     }
 }
 
-template <int R, bool OBS, bool GROW, int NSEG, bool FLAT>
+template <int R, bool OBS, bool GROW, int NSEG, int FLATM>
 void launch_march_n(const gca_alex_params& p, int E, int H, const uint8_t* gi, uint8_t* go, const int16_t* ai,
                     int16_t* ao, const uint8_t* vd, const uint16_t* db, const float* es, const int32_t* wi,
                     const uint32_t* rs, int32_t* counts, const uint8_t* act_in, uint8_t* act_out, MarchObs obs,
                     hipStream_t st) {
     const int nwaves = E * (H / SH) * NSEG;
     if constexpr (NSEG == 1)  // four independent tiles per workgroup
-        hipLaunchKernelGGL((alex_march_kernel<R, OBS, GROW, 1, FLAT>), dim3((unsigned)((nwaves + 3) / 4)), dim3(256), 0, st, p,
+        hipLaunchKernelGGL((alex_march_kernel<R, OBS, GROW, 1, FLATM>), dim3((unsigned)((nwaves + 3) / 4)), dim3(256), 0, st, p,
                            H, nwaves, gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs);
     else  // one strip (NSEG segment waves) per workgroup
-        hipLaunchKernelGGL((alex_march_kernel<R, OBS, GROW, NSEG, FLAT>), dim3((unsigned)(nwaves / NSEG)), dim3(64 * NSEG), 0,
+        hipLaunchKernelGGL((alex_march_kernel<R, OBS, GROW, NSEG, FLATM>), dim3((unsigned)(nwaves / NSEG)), dim3(64 * NSEG), 0,
                            st, p, H, nwaves, gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs);
 }
-template <int R, bool OBS, bool GROW, bool FLAT>
+template <int R, bool OBS, bool GROW, int FLATM>
 void launch_march_g(const gca_alex_params& p, int E, int H, int W, const uint8_t* gi, uint8_t* go, const int16_t* ai,
                     int16_t* ao, const uint8_t* vd, const uint16_t* db, const float* es, const int32_t* wi,
                     const uint32_t* rs, int32_t* counts, const uint8_t* act_in, uint8_t* act_out, MarchObs obs,
                     hipStream_t st) {
     if (W == MW)
-        launch_march_n<R, OBS, GROW, 1, FLAT>(p, E, H, gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs, st);
+        launch_march_n<R, OBS, GROW, 1, FLATM>(p, E, H, gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs, st);
     else if (W == 2 * MW)
-        launch_march_n<R, OBS, GROW, 2, FLAT>(p, E, H, gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs, st);
+        launch_march_n<R, OBS, GROW, 2, FLATM>(p, E, H, gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs, st);
     else
-        launch_march_n<R, OBS, GROW, 4, FLAT>(p, E, H, gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs, st);
+        launch_march_n<R, OBS, GROW, 4, FLATM>(p, E, H, gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs, st);
 }
 template <int R, bool OBS>
 void launch_march(const gca_alex_params& p, int E, int H, int W, const uint8_t* gi, uint8_t* go, const int16_t* ai,
                   int16_t* ao, const uint8_t* vd, const uint16_t* db, const float* es, const int32_t* wi,
                   const uint32_t* rs, int32_t* counts, const uint8_t* act_in, uint8_t* act_out, MarchObs obs,
                   hipStream_t st) {
+    // edge_slope NULL: flat terrain; vd NULL as well: uniform layers (march_impl checks the pairing)
     const bool grow = p.p_tree > 0.0f;
-    if (es && grow)
-        launch_march_g<R, OBS, true, false>(p, E, H, W, gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs, st);
-    else if (es)
-        launch_march_g<R, OBS, false, false>(p, E, H, W, gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs, st);
-    else if (grow)
-        launch_march_g<R, OBS, true, true>(p, E, H, W, gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs, st);
-    else
-        launch_march_g<R, OBS, false, true>(p, E, H, W, gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs, st);
+    const int fm = es ? 0 : (vd ? 1 : 2);
+#define GCA_MARCH_FM(FM)                                                                                                \
+    if (grow)                                                                                                         \
+        launch_march_g<R, OBS, true, FM>(p, E, H, W, gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs, st); \
+    else                                                                                                              \
+        launch_march_g<R, OBS, false, FM>(p, E, H, W, gi, go, ai, ao, vd, db, es, wi, rs, counts, act_in, act_out, obs, st);
+    if (fm == 0) {
+        GCA_MARCH_FM(0)
+    } else if (fm == 1) {
+        GCA_MARCH_FM(1)
+    } else {
+        GCA_MARCH_FM(2)
+    }
+#undef GCA_MARCH_FM
 }
 
 template <bool OBS>
@@ -1145,8 +1167,11 @@ int march_impl(const gca_alex_params* p, int E, int H, int W, const uint8_t* gri
                const int16_t* age_in, int16_t* age_out, const uint8_t* vd, const uint16_t* dous_bits,
                const float* edge_slope, const int32_t* wind_index, const uint32_t* rng_step, int32_t* counts,
                const uint8_t* act_in, uint8_t* act_out, MarchObs obs, void* stream) {
-    GCA_CHECK_ARG(p && grid_in && grid_out && age_in && age_out && vd && dous_bits && wind_index,
+    GCA_CHECK_ARG(p && grid_in && grid_out && age_in && age_out && dous_bits && wind_index,
                   "alex_step_march: null argument");  // edge_slope NULL: flat terrain (every slope factor 1)
+    GCA_CHECK_ARG(vd || (!edge_slope && p->vd_uniform >= 0 && p->vd_uniform <= 255 && (p->vd_uniform & 0x88) == 0),
+                  "alex_step_march: vd = NULL (uniform layers) needs edge_slope = NULL and p->vd_uniform = "
+                  "vegetation | density << 4 with both in 0..7");
     GCA_CHECK_ARG(E > 0 && H > 0 && (W == MW || W == 2 * MW || W == 4 * MW) && H % SH == 0,
                   "alex_step_march: W must be 256, 512 or 1024 and H a multiple of 16");
     GCA_CHECK_ARG(p->R >= 1 && p->R <= GCA_MAX_RADIUS, "alex_step_march: burn radius must be in [1, 8]");

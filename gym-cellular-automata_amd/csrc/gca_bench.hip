@@ -12,7 +12,8 @@
 //                             and writes the same 23.125 B / cell (+ 12 written with the frame) as the step, so its
 //                             time is the floor of that pattern on this device: kernel_ms / pattern_ms says how far the
 //                             step's instruction stream sits above it. edge_slopes = NULL: the flat-terrain step's
-//                             pattern (no slope planes: 7.125 B / cell, 4 waves / SIMD as that step).
+//                             pattern (no slope planes: 7.125 B / cell, 4 waves / SIMD as that step); vd = NULL too: the
+//                             uniform-layers step's (6.125 B / cell).
 #include "gca_common.h"
 
 typedef float gvf4 __attribute__((ext_vector_type(4)));
@@ -60,7 +61,7 @@ bench_march_pattern_kernel(int H, int nwaves, const uint8_t* __restrict__ g, uin
     const uint32_t HW = (uint32_t)H * W;
     const uint8_t* gE = g + (size_t)e * HW;
     const gvf4* sE = reinterpret_cast<const gvf4*>(FLAT ? es : es + (size_t)e * 4 * HW);
-    const uint8_t* vE = vd + (size_t)e * HW;
+    const uint8_t* vE = vd ? vd + (size_t)e * HW : vd;  // NULL: the uniform-layers step's pattern (no vd stream)
     const int16_t* aE = a + (size_t)e * HW;
     const uint16_t* dE = db + (size_t)e * (HW >> 4);
     uint32_t ring[NF];
@@ -85,7 +86,7 @@ bench_march_pattern_kernel(int H, int nwaves, const uint8_t* __restrict__ g, uin
         slopes(rs, sl[(sl_slot + 1) % 3]);
         const int rg = r + R + 1;
         gn[sl_slot & 1] = rg < H ? *reinterpret_cast<const uint32_t*>(gE + lo + (R + 1) * W) : 0u;
-        vv[sl_slot & 1] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(vE + lo));
+        vv[sl_slot & 1] = vd ? __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(vE + lo)) : 0u;
         dd[sl_slot & 1] = dE[lo >> 4];
         ag[sl_slot & 1] = __builtin_nontemporal_load(reinterpret_cast<const gvu2*>(aE + lo));
     };
@@ -147,7 +148,8 @@ static void launch_pattern(int E, int H, const uint8_t* g, uint8_t* go, const in
 extern "C" int gca_bench_march_pattern(int R, int E, int H, int W, const uint8_t* grid, uint8_t* grid_out,
                                        const int16_t* age, int16_t* age_out, const uint8_t* vd,
                                        const uint16_t* dous_bits, const float* edge_slopes, float* rgb, void* stream) {
-    GCA_CHECK_ARG(grid && grid_out && age && age_out && vd && dous_bits, "buffers required");
+    GCA_CHECK_ARG(grid && grid_out && age && age_out && dous_bits, "buffers required");
+    GCA_CHECK_ARG(vd || !edge_slopes, "vd = NULL (uniform layers) needs edge_slopes = NULL");
     GCA_CHECK_ARG(W == 256, "the pattern of the W = 256 marching step only");
     GCA_CHECK_ARG(E >= 1 && H >= 16 && H % 16 == 0, "E >= 1, H a multiple of 16");
     GCA_CHECK_ARG((int64_t)E * H * W < (int64_t)1 << 31, "E * H * W must stay below 2^31");

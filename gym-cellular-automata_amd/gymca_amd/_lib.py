@@ -83,6 +83,7 @@ class AlexParams(ctypes.Structure):
         ("winds", (c_float * 9) * 16),
         ("heat0", c_float),
         ("burnout_eq1", c_int32),
+        ("vd_uniform", c_int32),
     ]
 
 

@@ -234,6 +234,8 @@ class AdvancedForestFireBulldozerEnv:
         E, H, W = self.num_envs, self.nrows, self.ncols
         call("gca_alex_pack_layers", dev.ptr(self.vegetation), dev.ptr(self.density), dev.ptr(self.dousing),
              dev.ptr(self.vd), dev.ptr(self.dous_bits), E, H, W, dev.stream_ptr(self.device))
+        if hasattr(self, "flat_terrain"):  # (construction packs before the slopes exist; _slopes_from refreshes)
+            self.refresh_terrain()
 
     @property
     def march(self):
@@ -261,9 +263,19 @@ class AdvancedForestFireBulldozerEnv:
         """Re-derive `flat_terrain` from the slope buffer: True when every edge value is +-1, i.e. every slope factor of
         every env is exactly 1 (use_hidden=False: init_altitude_same gives zero slopes, exp_f32(0) = 1). The marching
         step then streams no slope planes (gca_alex_step_march with edge_slope = NULL; bit for bit the same step).
-        The env calls it whenever it sets the slopes (construction, set_state(altitude=...), adopted contexts); call it
-        after writing `slope_data` in place."""
+        On flat terrain `uniform_layers` says whether every cell of every env has the same packed vegetation / density
+        byte (use_hidden=False: init_vegetation_same / init_density_same); then the step reads no vd layer either (vd =
+        NULL, the byte in alex_params.vd_uniform). The env calls it whenever it sets the slopes or the layers
+        (construction, set_state(altitude= / vegetation= / density=), adopted contexts); call it after writing
+        `slope_data`, `vegetation`, `density` or `vd` in place."""
         self.flat_terrain = self.slope_layout != "planes" and bool((self.slope_data.abs() == 1.0).all())
+        self.uniform_layers = False
+        vd = getattr(self, "vd", None)
+        if self.flat_terrain and vd is not None:
+            v0 = int(vd.reshape(-1)[0])
+            if (v0 & 0x88) == 0 and bool((vd == v0).all()):
+                self.alex_params.vd_uniform = v0
+                self.uniform_layers = True
 
     def p_slope_planes(self):
         """The general 8-plane p_slope (E, 8, H, W) = exp_f32(0.078 * slope) of this env's altitude
@@ -683,9 +695,11 @@ class AdvancedForestFireBulldozerEnv:
         E, H, W = self.num_envs, self.nrows, self.ncols
         a, b = self.cur, 1 - self.cur
         if self.slope_layout == "packed":
+            flat = self.march and self.flat_terrain
             args = (self.alex_params, E, H, W, dev.ptr(self.grid[a]), dev.ptr(self.grid[b]),
-                    dev.ptr(self.age[a]), dev.ptr(self.age[b]), dev.ptr(self.vd), dev.ptr(self.dous_bits),
-                    dev.ptr(None if self.march and self.flat_terrain else self.slope_data), dev.ptr(self.wind_index),
+                    dev.ptr(self.age[a]), dev.ptr(self.age[b]),
+                    dev.ptr(None if flat and self.uniform_layers else self.vd), dev.ptr(self.dous_bits),
+                    dev.ptr(None if flat else self.slope_data), dev.ptr(self.wind_index),
                     dev.ptr(self.rng_step), dev.ptr(self.counts),
                     dev.ptr(None if self.act is None else self.act[a]), dev.ptr(None if self.act is None else self.act[b]))
             fn = "gca_alex_step_march" if self.march else "gca_alex_step_packed"

@@ -176,6 +176,9 @@ typedef struct {
     int32_t burnout_eq1;       /* 0: FIRE -> EMPTY iff age <= 1 (ca_alexandridis_jax.py:389);
                                   1: iff age == 1, i.e. the decremented age hits 0 (classic
                                   ca_alexandridis.py:181-183). Ages are decremented either way. */
+    int32_t vd_uniform;        /* gca_alex_step_march* with vd = NULL (uniform layers, flat terrain only): the packed
+                                  byte vegetation | density << 4 of every cell of every env (init_vegetation_same /
+                                  init_density_same, advanced_bulldozer.py:190-195); unused otherwise */
 } gca_alex_params;
 
 /* p_slope[e][d][r][c] = slope_factor(0.078f * slope[e][r][c][d']) for the 8 non-centre d'
@@ -239,7 +242,8 @@ int gca_alex_step_packed_rgb(const gca_alex_params* p, int E, int H, int W, cons
  * activity map and frame, except edge_slope: the edge layout (E,4,H,W) in natural column order (the output of
  * gca_alex_edge_slope_from_altitude, not coalesced), or NULL for flat terrain: every slope factor 1, as when every edge
  * value is +-1 (use_hidden=False: init_altitude_same, advanced_bulldozer.py:190-197, gives zero slopes) — no slope
- * planes are read (7.125 instead of 23.125 B / cell) and the results are those of the all-ones planes, bit for bit. */
+ * planes are read (7.125 instead of 23.125 B / cell) and the results are those of the all-ones planes, bit for bit.
+ * With edge_slope = NULL, vd may be NULL too: every cell's packed layer byte is p->vd_uniform (6.125 B / cell). */
 int gca_alex_step_march(const gca_alex_params* p, int E, int H, int W, const uint8_t* grid_in, uint8_t* grid_out,
                         const int16_t* age_in, int16_t* age_out, const uint8_t* vd, const uint16_t* dous_bits,
                         const float* edge_slope, const int32_t* wind_index, const uint32_t* rng_step, int32_t* counts,
@@ -485,8 +489,8 @@ int gca_ds_step(const uint8_t* grid_in, uint8_t* grid_out, int E, int H, int W, 
  * loads and stores: the practical HBM ceiling the bench reports beside the 8 TB/s spec.
  * gca_bench_march_pattern: the loads and stores of gca_alex_step_march at W = 256 (radius R in 4..7; with rgb != NULL
  * also the fused frame's f32 RGB stores) with trivial arithmetic, on the env's packed-layout buffers: the floor of
- * that access pattern on this device; edge_slopes = NULL: the flat-terrain step's pattern (no slope planes). Outputs are
- * scratch (their values mean nothing). */
+ * that access pattern on this device; edge_slopes = NULL: the flat-terrain step's pattern (no slope planes), and vd =
+ * NULL with it the uniform-layers step's (no vd layer either). Outputs are scratch (their values mean nothing). */
 int gca_bench_copy(const void* src, void* dst, int64_t nbytes, int nt, void* stream);
 int gca_bench_march_pattern(int R, int E, int H, int W, const uint8_t* grid, uint8_t* grid_out, const int16_t* age,
                             int16_t* age_out, const uint8_t* vd, const uint16_t* dous_bits, const float* edge_slopes,

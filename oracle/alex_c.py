@@ -16,7 +16,7 @@ class OracleAlexParams(ctypes.Structure):
                 ("seed", ctypes.c_uint64), ("env_offset", ctypes.c_int32), ("empty", ctypes.c_int32),
                 ("tree", ctypes.c_int32), ("fire", ctypes.c_int32), ("n_winds", ctypes.c_int32),
                 ("winds", (ctypes.c_float * 9) * 16), ("heat0", ctypes.c_float),
-                ("burnout_eq1", ctypes.c_int32)]
+                ("burnout_eq1", ctypes.c_int32), ("vd_uniform", ctypes.c_int32)]
 
 
 _lib = None

@@ -47,6 +47,7 @@ typedef struct {
     float winds[16][9];
     float heat0;
     int32_t burnout_eq1;
+    int32_t vd_uniform; /* gca.h; the oracle reads per-cell layers */
 } oracle_alex_params;
 
 /* ------------------------------------------------------------------ Philox4x32-10 */

@@ -69,8 +69,8 @@ def main():
         for name, sl, vd in (("const", const_slope, const_vd), ("rand_slope", rand_slope, const_vd),
                              ("rand_vd", const_slope, rand_vd), ("rand_both", rand_slope, rand_vd)):
             env.slope_data.copy_(sl)
-            env.refresh_terrain()  # "const" (all factors 1) runs the flat-terrain step since r06
             env.vd.copy_(vd)
+            env.refresh_terrain()  # "const" runs the flat-terrain / uniform-layers step since r06
             out.setdefault(name + "_ms", []).append(timed(step, restore))
             print(name, out[name + "_ms"][-1], file=sys.stderr, flush=True)
     dst = torch.empty_like(const_slope)

@@ -25,10 +25,13 @@ def main(E=4096, N=256, K=10, reps=5, rgb=False):
     st = dev.stream_ptr(device)
     assert bool((env.slope_data.abs() == 1.0).all())
 
-    def launch(flat):
+    assert env.uniform_layers
+
+    def launch(flat):  # flat: 0 general, 1 flat terrain, 2 flat + uniform layers
         a, b = env.cur, 1 - env.cur
         args = [env.alex_params, E, N, N, dev.ptr(env.grid[a]), dev.ptr(env.grid[b]), dev.ptr(env.age[a]),
-                dev.ptr(env.age[b]), dev.ptr(env.vd), dev.ptr(env.dous_bits), None if flat else dev.ptr(env.slope_data),
+                dev.ptr(env.age[b]), None if flat == 2 else dev.ptr(env.vd), dev.ptr(env.dous_bits),
+                None if flat else dev.ptr(env.slope_data),
                 dev.ptr(env.wind_index), dev.ptr(env.rng_step), dev.ptr(env.counts), None, None]
         if rgb:
             args += [dev.ptr(env.obs_colors), dev.ptr(env.is_night), dev.ptr(env.rgb)]
@@ -37,18 +40,18 @@ def main(E=4096, N=256, K=10, reps=5, rgb=False):
 
     out = {"E": E, "N": N, "K": K, "reps": reps, "rgb": rgb, "lib": os.environ.get("GCA_LIB_PATH", "default")}
     res = {}
-    for flat in (False, True):
+    for flat in (0, 1, 2):
         bench.synthetic_state(env, 0, device)
         for _ in range(3):
             launch(flat)
         torch.cuda.synchronize()
         res[flat] = (env.grid[env.cur].clone(), env.age[env.cur].clone(), env.counts.clone(),
                      env.rgb.clone() if rgb else None)
-    same = all(torch.equal(x, y) for x, y in zip(res[False], res[True]) if x is not None)
+    same = all(torch.equal(x, y) for f in (1, 2) for x, y in zip(res[0], res[f]) if x is not None)
     out["bit_exact"] = bool(same)
     del res
     for rep in range(2):
-        for flat in (False, True):
+        for flat in (0, 1, 2):
             times = []
             for _ in range(reps):
                 bench.synthetic_state(env, 0, device)
@@ -62,7 +65,7 @@ def main(E=4096, N=256, K=10, reps=5, rgb=False):
                 torch.cuda.synchronize()
                 times.append(e0.elapsed_time(e1) / K)
             times.sort()
-            out[("flat" if flat else "general") + f"_p{rep}_ms"] = round(times[len(times) // 2], 4)
+            out[("general", "flat", "flat_uniform")[flat] + f"_p{rep}_ms"] = round(times[len(times) // 2], 4)
     print(json.dumps(out), flush=True)
 
 

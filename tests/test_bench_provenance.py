@@ -28,13 +28,15 @@ def test_headline_key_names_the_launched_template():
     bench = _bench()
     p = types.SimpleNamespace(R=6, p_tree=0.0)
     env = types.SimpleNamespace(alex_params=p, march=True, slope_layout="packed", ncols=256)
-    assert bench.headline_kernel_key(env) == "alex_march<6, false, false, 1, false>"
+    assert bench.headline_kernel_key(env) == "alex_march<6, false, false, 1, 0>"
     p.p_tree = 0.5
-    assert bench.headline_kernel_key(env) == "alex_march<6, false, true, 1, false>"
+    assert bench.headline_kernel_key(env) == "alex_march<6, false, true, 1, 0>"
     env.ncols = 512
-    assert bench.headline_kernel_key(env) == "alex_march<6, false, true, 2, false>"
+    assert bench.headline_kernel_key(env) == "alex_march<6, false, true, 2, 0>"
     env.flat_terrain = True  # edge_slope = NULL: the flat-terrain instance
-    assert bench.headline_kernel_key(env) == "alex_march<6, false, true, 2, true>"
+    assert bench.headline_kernel_key(env) == "alex_march<6, false, true, 2, 1>"
+    env.uniform_layers = True  # vd = NULL too
+    assert bench.headline_kernel_key(env) == "alex_march<6, false, true, 2, 2>"
     env = types.SimpleNamespace(alex_params=types.SimpleNamespace(R=7, p_tree=0.0), march=False, slope_layout="packed")
     assert bench.headline_kernel_key(env) == "alex_step<7, 0, true, true, true, false>"
     env.slope_layout = "planes"

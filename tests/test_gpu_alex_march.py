@@ -355,12 +355,14 @@ def test_env_march_equals_tiled_at_wide_grids(device, N, pinecones):
                 env.conditional_reset()
 
 
+@pytest.mark.parametrize("uniform", [False, True])
 @pytest.mark.parametrize("R,W,p_tree,seed", [(6, 256, 0.0, 81), (1, 256, 0.01, 82), (8, 256, 0.0, 83), (7, 512, 0.0, 84),
                                              (3, 512, 0.01, 85), (6, 1024, 0.0, 86)])
-def test_flat_terrain_step_equals_unit_planes(device, R, W, p_tree, seed):
+def test_flat_terrain_step_equals_unit_planes(device, R, W, p_tree, seed, uniform):
     """edge_slope = NULL (the flat-terrain instance: no slope planes read, every row through the factor-free pass) equals
     the general step on all-ones edge planes, bit for bit: grid, ages, counts and tile map over three chained steps,
-    the fused frame at W = 256 (day and night), with and without the tile activity map."""
+    the fused frame at W = 256 (day and night), with and without the tile activity map. `uniform`: every cell's
+    vegetation / density the same (use_hidden=False's layers) and vd = NULL as well (p.vd_uniform)."""
     import torch
 
     from gymca_amd import _device as dev
@@ -370,8 +372,14 @@ def test_flat_terrain_step_equals_unit_planes(device, R, W, p_tree, seed):
     E, H = 3, 48
     case = make_case(E, H, W, seed, p_tree=p_tree, dousing_p=0.2, fire_p=0.05)
     p = _with_radius(params(H, p_tree, seed=seed * 3), R)
+    if uniform:
+        case["veg"][...] = 4
+        case["den"][...] = 2
+        p.vd_uniform = 4 | 2 << 4
     ones = torch.ones((E, 4, H, W), dtype=torch.float32, device=device)
     vd, bits = _layers(device, case)
+    if uniform:
+        assert bool((vd == p.vd_uniform).all())
     rgb = None
     if W == 256:
         col = torch.zeros((12, 4), dtype=torch.float32, device=device)
@@ -382,7 +390,7 @@ def test_flat_terrain_step_equals_unit_planes(device, R, W, p_tree, seed):
         for fn, extra in (("gca_alex_step_march", {}),) + ((("gca_alex_step_march_rgb", {"rgb": rgb}),) if rgb else ()):
             act = np.ones((E, H // 16), np.uint8) if (W == 256 and p_tree == 0.0) else None
             ref = _run(device, fn, p, case, ones, rs, vd, bits, act_in=act, **extra)
-            got = _run(device, fn, p, case, None, rs, vd, bits, act_in=act, **extra)
+            got = _run(device, fn, p, case, None, rs, None if uniform else vd, bits, act_in=act, **extra)
             for k in range(5):
                 if ref[k] is not None:
                     assert np.array_equal(got[k], ref[k]), (fn, s, k)
@@ -403,7 +411,7 @@ def test_env_flat_terrain_equals_general(device, extensions):
     E, N = 6, 256
     envs = [AdvancedForestFireBulldozerEnv(N, N, key=5, num_envs=E, use_hidden=False, device=device, observation="rgb",
                                            enable_extensions=extensions) for _ in range(2)]
-    assert all(env.flat_terrain for env in envs)
+    assert all(env.flat_terrain and env.uniform_layers for env in envs)
     envs[1].flat_terrain = False
     for env in envs:
         env.reset()
@@ -422,6 +430,11 @@ def test_env_flat_terrain_equals_general(device, extensions):
                 env.conditional_reset()
     assert int(envs[0].counts[:, 2].sum()) > 0
     env = envs[0]
+    env.set_state(vegetation=torch.full((E, N, N), 2, dtype=torch.uint8, device=device))
+    assert env.flat_terrain and env.uniform_layers and env.alex_params.vd_uniform == (2 | 3 << 4)
+    env.vegetation[0, 3, 3] = 5
+    env.set_state(vegetation=env.vegetation.clone())
+    assert env.flat_terrain and not env.uniform_layers
     env.slope_data[:, 0, 5, 5] = 1.5
     env.refresh_terrain()
-    assert not env.flat_terrain
+    assert not env.flat_terrain and not env.uniform_layers
