@@ -811,15 +811,21 @@ __global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_
                 asm volatile("" : "+v"(ph[0]), "+v"(ph[1]));
                 __builtin_amdgcn_sched_barrier(0);
             }
-            uint32_t D1[4], D2[4];
-            if constexpr (HALO) {
-                window4<true>(Dv1, 1, D1, WZ, xr[8]);
-                window4<true>(Dv2, 2, D2, WZ, xr[9]);
-            } else {
-                window4(Dv1, 1, D1, WZ);
-                window4(Dv2, 2, D2, WZ);
-            }
-            {  // the two pairs interleaved step by step (no packed result read by the next instruction)
+            // the dousing term only where the wave sees a doused cell in its 5 x 5 windows (the 5-row sums Dv2 contain
+            // the 3-row Dv1; HALO: the neighbour segments' edge sums too). Dousing is sparse (one bulldozer per env):
+            // most wave-rows skip the two windows. Skipping subtracts nothing instead of +-0, which can differ only in
+            // the sign of a zero heat; a zero heat gives every direction's factor +-0, which leaves qn unchanged either
+            // way, so the step's outputs are the same bit for bit
+            const bool dous_any = __ballot((Dv2 | (HALO ? xr[8] | xr[9] : 0u)) != 0u) != 0ull;
+            if (dous_any) {  // the two pairs interleaved step by step (no packed result read by the next instruction)
+                uint32_t D1[4], D2[4];
+                if constexpr (HALO) {
+                    window4<true>(Dv1, 1, D1, WZ, xr[8]);
+                    window4<true>(Dv2, 2, D2, WZ, xr[9]);
+                } else {
+                    window4(Dv1, 1, D1, WZ);
+                    window4(Dv2, 2, D2, WZ);
+                }
                 gca_f2 d1[2], d2[2], dz[2];
 #pragma unroll
                 for (int h = 0; h < 2; ++h) d1[h] = wsum_f2(D1[2 * h], D1[2 * h + 1]);

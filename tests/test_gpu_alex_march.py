@@ -438,3 +438,33 @@ def test_env_flat_terrain_equals_general(device, extensions):
     env.slope_data[:, 0, 5, 5] = 1.5
     env.refresh_terrain()
     assert not env.flat_terrain and not env.uniform_layers
+
+
+@pytest.mark.parametrize("W,R", [(256, 6), (512, 7), (1024, 8)])
+def test_march_sparse_dousing_equals_packed(device, W, R):
+    """Sparse dousing (most wave-rows see none in their 5 x 5 windows and skip the dousing term): the marching step,
+    general and flat terrain, equals the tiled packed step bit for bit; doused cells placed on the 256-column segment
+    edges (the HALO exchange carries their window sums across) and in the grid's first / last rows."""
+    case = make_case(3, 48, W, 90 + R, p_tree=0.0, dousing_p=0.0, fire_p=0.08)
+    d = case["dous"]
+    d[0, 10, 255] = d[0, 30, 256 % W] = d[1, 0, 5] = d[1, 47, W - 1] = d[2, 20, 128] = 1
+    if W > 256:
+        d[2, 5, 511] = d[2, 6, 512 % W] = d[0, 40, 254] = 1
+    p = _with_radius(params(48, 0.0, seed=R), R)
+    es, _ = slopes(device, altitude(3, 48, W, 90 + R))
+    coal = _coalesced(device, es)
+    vd, bits = _layers(device, case)
+    import torch
+
+    ones = torch.ones_like(es)
+    ones_coal = _coalesced(device, ones)
+    for s in range(3):
+        rs = np.full(3, 4 * s + 1, np.uint32)
+        g0, a0, c0, _, _ = _run(device, "gca_alex_step_packed", p, case, coal, rs, vd, bits)
+        g1, a1, c1, _, _ = _run(device, "gca_alex_step_march", p, case, es, rs, vd, bits)
+        assert np.array_equal(g1, g0) and np.array_equal(a1, a0) and np.array_equal(c1, c0), s
+        f0 = _run(device, "gca_alex_step_packed", p, case, ones_coal, rs, vd, bits)
+        f1 = _run(device, "gca_alex_step_march", p, case, None, rs, vd, bits)
+        for k in range(3):
+            assert np.array_equal(f1[k], f0[k]), (s, k)
+        case["grid"], case["age"] = g1, a1
