@@ -34,6 +34,9 @@
 #ifndef GCA_MARCH_FLAT_OCC
 #define GCA_MARCH_FLAT_OCC 4  // waves / SIMD of the flat-terrain step (no slope planes in registers: ~110 VGPRs)
 #endif
+#ifndef GCA_MARCH_OBS_FLAT_OCC
+#define GCA_MARCH_OBS_FLAT_OCC 3  // waves / SIMD of the flat-terrain step with the fused frame (r06: 2 -> 3, -18 %)
+#endif
 #ifndef GCA_MARCH_XROW
 #define GCA_MARCH_XROW 1  // the 17th slope row of a tile from the next tile's wave through LDS (r06; 0: from HBM again)
 #endif
@@ -227,7 +230,7 @@ template <int R, bool OBS, bool GROW, int NSEG, int FLATM>  // GROW: p_tree > 0 
 // occupancy: 3 waves / SIMD for the step (VGPR-bound, <= 168; 4 would spill), 2 for the fused frame: its 3 KiB per
 // wave-row of f32 RGB stores run faster from fewer concurrent waves (r05g, same box: 1.760 -> 1.723 ms per 4096 x 256^2
 // step with the frame; the plain step at 2 waves: +8 %)
-__global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_waves_per_eu(OBS ? 2 : (FLATM ? GCA_MARCH_FLAT_OCC : 3), OBS ? 2 : (FLATM ? GCA_MARCH_FLAT_OCC : 3)))) void alex_march_kernel(
+__global__ __launch_bounds__(NSEG == 1 ? 256 : 64 * NSEG) __attribute__((amdgpu_waves_per_eu(OBS ? (FLATM ? GCA_MARCH_OBS_FLAT_OCC : 2) : (FLATM ? GCA_MARCH_FLAT_OCC : 3), OBS ? (FLATM ? GCA_MARCH_OBS_FLAT_OCC : 2) : (FLATM ? GCA_MARCH_FLAT_OCC : 3)))) void alex_march_kernel(
     gca_alex_params p, int H, int nwaves, const uint8_t* __restrict__ grid_in, uint8_t* __restrict__ grid_out,
     const int16_t* age_in, int16_t* age_out,  // no __restrict__: the env updates ages in place
     const uint8_t* __restrict__ vd, const uint16_t* __restrict__ dbits, const float* __restrict__ es,

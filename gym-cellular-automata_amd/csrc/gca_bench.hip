@@ -12,7 +12,7 @@
 //                             and writes the same 23.125 B / cell (+ 12 written with the frame) as the step, so its
 //                             time is the floor of that pattern on this device: kernel_ms / pattern_ms says how far the
 //                             step's instruction stream sits above it. edge_slopes = NULL: the flat-terrain step's
-//                             pattern (no slope planes: 7.125 B / cell, 4 waves / SIMD as that step); vd = NULL too: the
+//                             pattern (no slope planes: 7.125 B / cell, 4 waves / SIMD as that step, 3 with the frame); vd = NULL too: the
 //                             uniform-layers step's (6.125 B / cell).
 #include "gca_common.h"
 
@@ -46,7 +46,7 @@ extern "C" int gca_bench_copy(const void* src, void* dst, int64_t nbytes, int nt
 }
 
 template <int R, bool FRAME, bool FLAT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FRAME ? 2 : (FLAT ? 4 : 3), FRAME ? 2 : (FLAT ? 4 : 3)))) void
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FRAME ? (FLAT ? 3 : 2) : (FLAT ? 4 : 3), FRAME ? (FLAT ? 3 : 2) : (FLAT ? 4 : 3)))) void
 bench_march_pattern_kernel(int H, int nwaves, const uint8_t* __restrict__ g, uint8_t* __restrict__ go,
                            const int16_t* __restrict__ a, int16_t* __restrict__ ao, const uint8_t* __restrict__ vd,
                            const uint16_t* __restrict__ db, const float* __restrict__ es, gvf4* __restrict__ rgb) {
