@@ -227,15 +227,16 @@ class AdvancedForestFireBulldozerEnv:
         self.act = (torch.ones((2, E, (H // 16) * (W // 256)), dtype=torch.uint8, device=self.device)
                     if on and not self.march else None)
 
-    def _pack_layers(self):
-        """vd and dousing bits of the packed layout from the u8 layers (no-op for the other layouts)."""
+    def _pack_layers(self, layers=True):
+        """vd and dousing bits of the packed layout from the u8 layers (no-op for the other layouts); `layers`:
+        vegetation / density may have changed (uniform_layers is re-derived), not only the dousing."""
         if self.vd is None:
             return
         E, H, W = self.num_envs, self.nrows, self.ncols
         call("gca_alex_pack_layers", dev.ptr(self.vegetation), dev.ptr(self.density), dev.ptr(self.dousing),
              dev.ptr(self.vd), dev.ptr(self.dous_bits), E, H, W, dev.stream_ptr(self.device))
-        if hasattr(self, "flat_terrain"):  # (construction packs before the slopes exist; _slopes_from refreshes)
-            self.refresh_terrain()
+        if layers and hasattr(self, "flat_terrain"):  # (construction packs before the slopes; _slopes_from refreshes)
+            self._refresh_layers()
 
     @property
     def march(self):
@@ -267,8 +268,12 @@ class AdvancedForestFireBulldozerEnv:
         byte (use_hidden=False: init_vegetation_same / init_density_same); then the step reads no vd layer either (vd =
         NULL, the byte in alex_params.vd_uniform). The env calls it whenever it sets the slopes or the layers
         (construction, set_state(altitude= / vegetation= / density=), adopted contexts); call it after writing
-        `slope_data`, `vegetation`, `density` or `vd` in place."""
+        `slope_data` or `vd` in place (new vegetation / density go through set_state, which repacks vd)."""
         self.flat_terrain = self.slope_layout != "planes" and bool((self.slope_data.abs() == 1.0).all())
+        self._refresh_layers()
+
+    def _refresh_layers(self):
+        """`uniform_layers` from the packed vd layer (flat terrain only; see refresh_terrain)."""
         self.uniform_layers = False
         vd = getattr(self, "vd", None)
         if self.flat_terrain and vd is not None:
@@ -395,7 +400,7 @@ class AdvancedForestFireBulldozerEnv:
             self.altitude = alt.to(self.device, torch.float64).contiguous()
             self._slopes_from(self.altitude)
         if vegetation is not None or density is not None or dousing is not None:
-            self._pack_layers()
+            self._pack_layers(layers=vegetation is not None or density is not None)
         if self.act is not None:  # the state may have fire anywhere now
             self.act.fill_(1)
         call("gca_count_cells", dev.ptr(self.grid[self.cur]), E, H, W, self._empty, self._tree, self._fire,
@@ -548,7 +553,7 @@ class AdvancedForestFireBulldozerEnv:
         if shared:
             self._apply_shared(shared)
         if {"vegetation", "density", "dousing_count"} & touched:
-            self._pack_layers()
+            self._pack_layers(layers=bool({"vegetation", "density"} & touched))
         if "true_grid" in touched:
             if self.act is not None:
                 self.act.fill_(1)
