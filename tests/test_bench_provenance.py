@@ -70,3 +70,18 @@ def test_profile_entry_requires_the_same_sources(tmp_path, monkeypatch):
     # not the profiled workload -> null
     e, info = bench.profile_entry(types.SimpleNamespace(envs=1024, size=256), key)
     assert e is None
+
+
+def test_algorithmic_bytes_follow_the_launched_instance():
+    """roofline.algorithmic_bytes_per_cell is that of the step the env launches: the packed layout's 23.125 B, minus the
+    16 B of slope planes on flat terrain, minus the layer byte with uniform layers (tiled / other layouts unchanged)."""
+    bench = _bench()
+    env = types.SimpleNamespace(march=True, flat_terrain=False, uniform_layers=False)
+    assert bench.alex_bytes(env, "packed") == 23.125
+    env.flat_terrain = True
+    assert bench.alex_bytes(env, "packed") == 7.125
+    env.uniform_layers = True
+    assert bench.alex_bytes(env, "packed") == 6.125
+    env.march = False  # the tiled step reads every plane
+    assert bench.alex_bytes(env, "packed") == 23.125
+    assert bench.alex_bytes(types.SimpleNamespace(), "planes") == 41
