@@ -1,7 +1,7 @@
 """Static VALU instructions of one gca_alex_march.hip kernel instance by source line (ISA analysis; no GPU).
 Compiles the R = 6 instances only (-DGCA_MARCH_ANALYSIS_R6) to device assembly with line info and counts, for the
 instance named by its template flags, the VALU instructions attributed to each source line, largest first.
-Usage: python scripts/isa_rows.py [OBS GROW NSEG FLAT] (default 0 0 1 1: the flat-terrain headline step)."""
+Usage: python scripts/isa_rows.py [OBS GROW NSEG FLATM] (default 0 0 1 2: the headline step, flat terrain + uniform layers)."""
 import collections
 import os
 import re
@@ -18,7 +18,7 @@ def main(obs=0, grow=0, nseg=1, flat=1, top=40):
                     "-munsafe-fp-atomics", "-DGCA_MARCH_ANALYSIS_R6", "--cuda-device-only", "-S", SRC, "-o", out],
                    check=True, stderr=subprocess.DEVNULL)
     L = open(out).read().split("\n")
-    name = f"alex_march_kernelILi6ELb{obs}ELb{grow}ELi{nseg}ELb{flat}E"
+    name = f"alex_march_kernelILi6ELb{obs}ELb{grow}ELi{nseg}ELi{flat}E"
     s = next(i for i, l in enumerate(L) if l.startswith("_Z") and name in l.split(":")[0])
     e = next(i for i in range(s, len(L)) if L[i].strip().startswith("s_endpgm"))
     files = {}
@@ -46,5 +46,5 @@ def main(obs=0, grow=0, nseg=1, flat=1, top=40):
 
 
 if __name__ == "__main__":
-    a = [int(x) for x in sys.argv[1:5]] if len(sys.argv) >= 5 else [0, 0, 1, 1]
+    a = [int(x) for x in sys.argv[1:5]] if len(sys.argv) >= 5 else [0, 0, 1, 2]
     main(*a)
