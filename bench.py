@@ -1377,6 +1377,9 @@ def main():
                          "survey_equiv_gbs": alex["survey_equiv_gbs"],
                          "survey_equiv_frac": alex["survey_equiv_gbs"] / HBM_PEAK_GBS,
                          "valu_busy": valu_busy,
+                         # what binds the timed kernel by its matched profile: VALU issue when the SIMDs are >= 95 % busy
+                         # (the flat-terrain step), else the HBM stream (its frac above says how close)
+                         "limiter": (None if valu_busy is None else "valu" if valu_busy >= 0.95 else "hbm"),
                          "profile": prof_info,
                          "slope_layout": args.slope_layout,
                          "moved_bytes_per_cell": alex["bytes_per_cell"],
